@@ -1,0 +1,568 @@
+// gprx_api.hip -- C ABI (include/gprx.h) over the gfx950 kernels: context/stream ownership,
+// batch workspaces in HBM, the per-evaluation launch sequence, status mapping, profiling.
+#include <cfloat>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/gprx.h"
+#include "gprx_internal.h"
+
+using gprx::DevBatch;
+using gprx::TS;
+
+namespace {
+
+struct KStat {
+  double ms = 0.0, flops = 0.0, bytes = 0.0;
+  int64_t n = 0;
+};
+struct PendingEv {
+  std::string name;
+  hipEvent_t a, b;
+  double flops, bytes;
+};
+
+}  // namespace
+
+struct gprx_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  std::string err;
+  int dist_mode = GPRX_DIST_EXPANDED;
+  bool prof = false;
+  std::map<std::string, KStat> stats;
+  std::vector<hipEvent_t> evpool;
+  std::vector<PendingEv> pending;
+};
+
+struct gprx_batch {
+  gprx_ctx* ctx = nullptr;
+  DevBatch db{};
+  std::vector<void*> allocs;
+  double* h_params = nullptr;  // pinned
+  double* h_out = nullptr;     // pinned, B*(d+3)
+  double* h_mu = nullptr;      // pinned, B*Mpad
+  double* h_var = nullptr;
+  int* h_status = nullptr;  // pinned, 2B (status, info)
+  bool factored = false;
+  bool have_train = false;
+  bool have_test = false;
+};
+
+struct gprx_gp {
+  gprx_batch* batch = nullptr;
+  int M_cap = 0;
+};
+
+namespace {
+
+int set_err(gprx_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+#define HIPCHK(ctx, expr)                                                                          \
+  do {                                                                                             \
+    hipError_t e_ = (expr);                                                                        \
+    if (e_ != hipSuccess)                                                                          \
+      return set_err((ctx), e_ == hipErrorOutOfMemory ? GPRX_OUT_OF_MEMORY : GPRX_DEVICE_ERROR,     \
+                     std::string(#expr) + ": " + hipGetErrorString(e_));                           \
+  } while (0)
+
+hipEvent_t ev_get(gprx_ctx* c) {
+  if (!c->evpool.empty()) {
+    hipEvent_t e = c->evpool.back();
+    c->evpool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  (void)hipEventCreate(&e);
+  return e;
+}
+
+// Launch helper: optional HIP-event bracket per launch, on the context stream.
+template <class F>
+void timed(gprx_ctx* c, const char* name, double flops, double bytes, F&& f) {
+  if (!c->prof) {
+    f();
+    return;
+  }
+  hipEvent_t a = ev_get(c), b = ev_get(c);
+  (void)hipEventRecord(a, c->stream);
+  f();
+  (void)hipEventRecord(b, c->stream);
+  c->pending.push_back({name, a, b, flops, bytes});
+}
+
+void collect(gprx_ctx* c) {
+  for (auto& p : c->pending) {
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, p.a, p.b);
+    KStat& s = c->stats[p.name];
+    s.ms += ms;
+    s.n += 1;
+    s.flops += p.flops;
+    s.bytes += p.bytes;
+    c->evpool.push_back(p.a);
+    c->evpool.push_back(p.b);
+  }
+  c->pending.clear();
+}
+
+template <class T>
+int dalloc(gprx_batch* b, T** p, size_t count) {
+  void* q = nullptr;
+  if (count == 0) count = 1;
+  hipError_t e = hipMalloc(&q, count * sizeof(T));
+  if (e != hipSuccess) {
+    *p = nullptr;
+    return set_err(b->ctx, e == hipErrorOutOfMemory ? GPRX_OUT_OF_MEMORY : GPRX_DEVICE_ERROR,
+                   std::string("hipMalloc: ") + hipGetErrorString(e));
+  }
+  b->allocs.push_back(q);
+  *p = (T*)q;
+  return GPRX_OK;
+}
+
+void free_test(gprx_batch* b);
+
+int alloc_test(gprx_batch* b, int M_max) {
+  DevBatch& db = b->db;
+  db.M = 0;
+  db.Mpad = ((M_max + TS - 1) / TS) * TS;
+  if (db.Mpad == 0) db.Mpad = TS;
+  db.mt = db.Mpad / TS;
+  const size_t B = db.B;
+  int rc;
+  if ((rc = dalloc(b, &db.Xs, B * db.Mpad * db.d))) return rc;
+  if ((rc = dalloc(b, &db.KsT, B * (size_t)db.Npad * db.Mpad))) return rc;
+  if ((rc = dalloc(b, &db.mu_part, B * db.nt * (size_t)db.Mpad))) return rc;
+  if ((rc = dalloc(b, &db.var_part, B * db.nt * (size_t)db.Mpad))) return rc;
+  if ((rc = dalloc(b, &db.out_mu, B * db.Mpad))) return rc;
+  if ((rc = dalloc(b, &db.out_var, B * db.Mpad))) return rc;
+  if (hipHostMalloc((void**)&b->h_mu, B * db.Mpad * sizeof(double)) != hipSuccess) return GPRX_OUT_OF_MEMORY;
+  if (hipHostMalloc((void**)&b->h_var, B * db.Mpad * sizeof(double)) != hipSuccess) return GPRX_OUT_OF_MEMORY;
+  (void)hipMemset(db.Xs, 0, B * db.Mpad * db.d * sizeof(double));
+  return GPRX_OK;
+}
+
+void release_ptr(gprx_batch* b, void* p) {
+  for (auto it = b->allocs.begin(); it != b->allocs.end(); ++it)
+    if (*it == p) {
+      (void)hipFree(p);
+      b->allocs.erase(it);
+      return;
+    }
+}
+
+void free_test(gprx_batch* b) {
+  DevBatch& db = b->db;
+  void* ps[] = {db.Xs, db.KsT, db.mu_part, db.var_part, db.out_mu, db.out_var};
+  for (void* p : ps)
+    if (p) release_ptr(b, p);
+  db.Xs = db.KsT = db.mu_part = db.var_part = db.out_mu = db.out_var = nullptr;
+  if (b->h_mu) (void)hipHostFree(b->h_mu);
+  if (b->h_var) (void)hipHostFree(b->h_var);
+  b->h_mu = b->h_var = nullptr;
+}
+
+int copy_in(gprx_ctx* c, void* dst, const void* src, size_t bytes, int mem) {
+  HIPCHK(c, hipMemcpyAsync(dst, src, bytes, mem == GPRX_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
+                           c->stream));
+  return GPRX_OK;
+}
+
+int run_predict_kernels(gprx_batch* b) {
+  gprx_ctx* c = b->ctx;
+  const DevBatch& db = b->db;
+  const double N = db.N, M = db.M, d = db.d, B = db.B;
+  timed(c, "pred_cross", B * (3.0 * N * M * d + 2.0 * N * M), B * 8.0 * (N * db.Mpad + (N + M) * d),
+        [&] { gprx::launch_pred_cross(db, c->stream); });
+  timed(c, "pred_var", B * N * N * M, B * 8.0 * (N * N / 2 + N * db.Mpad),
+        [&] { gprx::launch_pred_var(db, c->stream); });
+  timed(c, "pred_final", B * 2.0 * db.nt * db.Mpad, B * 16.0 * db.nt * db.Mpad,
+        [&] { gprx::launch_pred_final(db, c->stream); });
+  return GPRX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gprx_abi_version(void) { return GPRX_ABI_VERSION; }
+
+const char* gprx_status_string(int s) {
+  switch (s) {
+    case GPRX_OK: return "ok";
+    case GPRX_NOT_POSITIVE_DEFINITE: return "not positive definite";
+    case GPRX_INVALID_ARGUMENT: return "invalid argument";
+    case GPRX_DEVICE_ERROR: return "device error";
+    case GPRX_OUT_OF_MEMORY: return "out of memory";
+    case GPRX_NOT_READY: return "not ready";
+  }
+  return "unknown";
+}
+
+int gprx_ctx_create(int device, gprx_ctx** out) {
+  if (!out) return GPRX_INVALID_ARGUMENT;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return GPRX_DEVICE_ERROR;
+  if (device < 0 || device >= n) return GPRX_INVALID_ARGUMENT;
+  gprx_ctx* c = new gprx_ctx();
+  c->device = device;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return GPRX_DEVICE_ERROR;
+  }
+  *out = c;
+  return GPRX_OK;
+}
+
+void gprx_ctx_destroy(gprx_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  for (auto& p : c->pending) {
+    (void)hipEventDestroy(p.a);
+    (void)hipEventDestroy(p.b);
+  }
+  for (auto e : c->evpool) (void)hipEventDestroy(e);
+  (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+const char* gprx_ctx_last_error(const gprx_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int gprx_ctx_set_dist_mode(gprx_ctx* c, int mode) {
+  if (!c || (mode != GPRX_DIST_EXPANDED && mode != GPRX_DIST_DIRECT)) return GPRX_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->dist_mode = mode;
+  return GPRX_OK;
+}
+
+int gprx_ctx_device(const gprx_ctx* c) { return c ? c->device : -1; }
+
+int gprx_ctx_set_profiling(gprx_ctx* c, int enable) {
+  if (!c) return GPRX_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->prof = enable != 0;
+  return GPRX_OK;
+}
+
+int gprx_ctx_kernel_stats(gprx_ctx* c, const char* kernel, double* total_ms, int64_t* launches, double* algo_flops,
+                          double* algo_bytes) {
+  if (!c || !kernel) return GPRX_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> g(c->mu);
+  auto it = c->stats.find(kernel);
+  KStat s = it == c->stats.end() ? KStat() : it->second;
+  if (total_ms) *total_ms = s.ms;
+  if (launches) *launches = s.n;
+  if (algo_flops) *algo_flops = s.flops;
+  if (algo_bytes) *algo_bytes = s.bytes;
+  return GPRX_OK;
+}
+
+int gprx_ctx_reset_stats(gprx_ctx* c) {
+  if (!c) return GPRX_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->stats.clear();
+  return GPRX_OK;
+}
+
+int gprx_batch_create(gprx_ctx* c, int B, int d, int N, int M_max, gprx_batch** out) {
+  if (!c || !out) return GPRX_INVALID_ARGUMENT;
+  *out = nullptr;
+  if (B < 1 || d < 1 || d > gprx::DMAX || N < 1 || M_max < 0)
+    return set_err(c, GPRX_INVALID_ARGUMENT, "gprx_batch_create: need B>=1, 1<=d<=64, N>=1, M_max>=0");
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess) return GPRX_DEVICE_ERROR;
+  gprx_batch* b = new gprx_batch();
+  b->ctx = c;
+  DevBatch& db = b->db;
+  db.B = B;
+  db.d = d;
+  db.N = N;
+  db.Npad = ((N + TS - 1) / TS) * TS;
+  db.nt = db.Npad / TS;
+  db.ntl = db.nt * (db.nt + 1) / 2;
+  db.ld = db.Npad;
+  db.mat = (size_t)db.Npad * db.Npad;
+  db.pst = d + 4;
+  db.gps = d + 2;
+  const size_t Bs = B;
+  int rc = GPRX_OK;
+  auto fail = [&](int r) {
+    gprx_batch_destroy(b);
+    return r;
+  };
+  if ((rc = dalloc(b, &db.X, Bs * db.Npad * d))) return fail(rc);
+  if ((rc = dalloc(b, &db.Y, Bs * db.Npad))) return fail(rc);
+  if ((rc = dalloc(b, &db.K, Bs * db.mat))) return fail(rc);
+  if ((rc = dalloc(b, &db.Linv, Bs * db.mat))) return fail(rc);
+  if ((rc = dalloc(b, &db.Mt, Bs * db.mat))) return fail(rc);
+  if ((rc = dalloc(b, &db.z, Bs * db.Npad))) return fail(rc);
+  if ((rc = dalloc(b, &db.alpha, Bs * db.Npad))) return fail(rc);
+  if ((rc = dalloc(b, &db.params, Bs * db.pst))) return fail(rc);
+  if ((rc = dalloc(b, &db.logdet_part, Bs * db.nt))) return fail(rc);
+  if ((rc = dalloc(b, &db.grad_part, Bs * db.ntl * db.gps))) return fail(rc);
+  if ((rc = dalloc(b, &db.out, Bs * (d + 3)))) return fail(rc);
+  if ((rc = dalloc(b, &db.status, 2 * Bs))) return fail(rc);
+  db.info = db.status + Bs;
+  if ((rc = alloc_test(b, M_max))) return fail(rc);
+  if (hipHostMalloc((void**)&b->h_params, Bs * db.pst * sizeof(double)) != hipSuccess ||
+      hipHostMalloc((void**)&b->h_out, Bs * (d + 3) * sizeof(double)) != hipSuccess ||
+      hipHostMalloc((void**)&b->h_status, 2 * Bs * sizeof(int)) != hipSuccess)
+    return fail(set_err(c, GPRX_OUT_OF_MEMORY, "hipHostMalloc failed"));
+  // zero padding of X / Y (pad columns never enter a result; kept finite)
+  if (hipMemset(db.X, 0, Bs * db.Npad * d * sizeof(double)) != hipSuccess ||
+      hipMemset(db.Y, 0, Bs * db.Npad * sizeof(double)) != hipSuccess)
+    return fail(GPRX_DEVICE_ERROR);
+  *out = b;
+  return GPRX_OK;
+}
+
+void gprx_batch_destroy(gprx_batch* b) {
+  if (!b) return;
+  if (b->ctx) (void)hipSetDevice(b->ctx->device);
+  if (b->ctx) (void)hipStreamSynchronize(b->ctx->stream);
+  for (void* p : b->allocs) (void)hipFree(p);
+  if (b->h_params) (void)hipHostFree(b->h_params);
+  if (b->h_out) (void)hipHostFree(b->h_out);
+  if (b->h_mu) (void)hipHostFree(b->h_mu);
+  if (b->h_var) (void)hipHostFree(b->h_var);
+  if (b->h_status) (void)hipHostFree(b->h_status);
+  delete b;
+}
+
+int gprx_batch_dims(const gprx_batch* b, int* B, int* d, int* N, int* M_max) {
+  if (!b) return GPRX_INVALID_ARGUMENT;
+  if (B) *B = b->db.B;
+  if (d) *d = b->db.d;
+  if (N) *N = b->db.N;
+  if (M_max) *M_max = b->db.Mpad;
+  return GPRX_OK;
+}
+
+int gprx_batch_set_train(gprx_batch* b, const double* X, int64_t xs, const double* Y, int64_t ys, int mem) {
+  if (!b || !X || !Y || xs < 0 || ys < 0) return GPRX_INVALID_ARGUMENT;
+  gprx_ctx* c = b->ctx;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess) return GPRX_DEVICE_ERROR;
+  DevBatch& db = b->db;
+  int rc;
+  for (int s = 0; s < db.B; ++s) {
+    // X slot: d x N contiguous (column t = CState t) -> d x Npad (tail zero)
+    if ((rc = copy_in(c, db.X + (size_t)s * db.Npad * db.d, X + (size_t)s * xs, (size_t)db.N * db.d * sizeof(double), mem)))
+      return rc;
+    if ((rc = copy_in(c, db.Y + (size_t)s * db.Npad, Y + (size_t)s * ys, (size_t)db.N * sizeof(double), mem))) return rc;
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  b->have_train = true;
+  b->factored = false;
+  return GPRX_OK;
+}
+
+int gprx_batch_set_test(gprx_batch* b, const double* Xs, int M, int64_t xss, int mem) {
+  if (!b || (!Xs && M > 0) || M < 0 || xss < 0) return GPRX_INVALID_ARGUMENT;
+  gprx_ctx* c = b->ctx;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess) return GPRX_DEVICE_ERROR;
+  DevBatch& db = b->db;
+  if (M > db.Mpad) {
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    free_test(b);
+    int rc = alloc_test(b, M);
+    if (rc) return rc;
+  }
+  HIPCHK(c, hipMemsetAsync(db.Xs, 0, (size_t)db.B * db.Mpad * db.d * sizeof(double), c->stream));
+  int rc;
+  for (int s = 0; s < db.B && M > 0; ++s)
+    if ((rc = copy_in(c, db.Xs + (size_t)s * db.Mpad * db.d, Xs + (size_t)s * xss, (size_t)M * db.d * sizeof(double), mem)))
+      return rc;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  db.M = M;
+  b->have_test = M > 0;
+  return GPRX_OK;
+}
+
+static int batch_predict_locked(gprx_batch* b, double* mu, double* var) {
+  gprx_ctx* c = b->ctx;
+  DevBatch& db = b->db;
+  if (!b->factored) return set_err(c, GPRX_NOT_READY, "predict before a successful factorisation");
+  if (!b->have_test || db.M == 0) return GPRX_OK;
+  int rc = run_predict_kernels(b);
+  if (rc) return rc;
+  HIPCHK(c, hipMemcpyAsync(b->h_mu, db.out_mu, (size_t)db.B * db.Mpad * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(b->h_var, db.out_var, (size_t)db.B * db.Mpad * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  collect(c);
+  for (int s = 0; s < db.B; ++s) {
+    if (mu) memcpy(mu + (size_t)s * db.M, b->h_mu + (size_t)s * db.Mpad, db.M * sizeof(double));
+    if (var) memcpy(var + (size_t)s * db.M, b->h_var + (size_t)s * db.Mpad, db.M * sizeof(double));
+  }
+  return GPRX_OK;
+}
+
+int gprx_batch_run(gprx_batch* b, const double* theta, unsigned flags, double* mll, double* grad, double* mu,
+                   double* var, int* status, int* info) {
+  if (!b || !theta) return GPRX_INVALID_ARGUMENT;
+  gprx_ctx* c = b->ctx;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!b->have_train) return set_err(c, GPRX_INVALID_ARGUMENT, "gprx_batch_run before gprx_batch_set_train");
+  if (hipSetDevice(c->device) != hipSuccess) return GPRX_DEVICE_ERROR;
+  DevBatch& db = b->db;
+  db.dist_mode = c->dist_mode;
+  const int d = db.d, B = db.B, np = d + 2;
+  // hyper-parameters -> kernel parameters, exactly as SEArd / GPE derive them:
+  //   il2 = exp(-2 log ell), sf2 = exp(2 log sf), noise = exp(2 logNoise) + eps()
+  for (int s = 0; s < B; ++s) {
+    const double* th = theta + (size_t)s * np;
+    double* P = b->h_params + (size_t)s * db.pst;
+    bool finite = true;
+    for (int q = 0; q < np; ++q) finite = finite && std::isfinite(th[q]);
+    b->h_status[s] = finite ? 0 : GPRX_INVALID_ARGUMENT;
+    b->h_status[B + s] = 0;
+    for (int p = 0; p < d; ++p) P[p] = finite ? std::exp(-2.0 * th[1 + p]) : 1.0;
+    P[d] = finite ? std::exp(2.0 * th[d + 1]) : 1.0;
+    const double sn2 = finite ? std::exp(2.0 * th[0]) : 1.0;
+    P[d + 1] = sn2 + DBL_EPSILON;
+    P[d + 2] = sn2;
+    P[d + 3] = 0.0;
+  }
+  HIPCHK(c, hipMemcpyAsync(db.params, b->h_params, (size_t)B * db.pst * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(db.status, b->h_status, 2 * (size_t)B * sizeof(int), hipMemcpyHostToDevice, c->stream));
+  const double T3 = (double)TS * TS * TS, Bd = B, nt = db.nt, Np = db.Npad;
+  timed(c, "gram", Bd * 3.0 * db.N * (double)db.N * d / 2.0, Bd * 8.0 * (Np * Np / 2.0 + Np * d),
+        [&] { gprx::launch_gram(db, c->stream); });
+  for (int j = 0; j < db.nt; ++j) {
+    if (j > 0)
+      timed(c, "potrf_update", Bd * (2.0 * T3 * j * (nt - j) - T3 * j),
+            Bd * 8.0 * TS * TS * (2.0 * (nt - j) + j * (nt - j + 1.0)),
+            [&] { gprx::launch_potrf_update(db, j, c->stream); });
+    timed(c, "potrf_diag", Bd * (T3 / 3.0 + T3 / 3.0), Bd * 8.0 * TS * TS * 4.0,
+          [&] { gprx::launch_potrf_diag(db, j, c->stream); });
+    if (j < db.nt - 1)
+      timed(c, "trsm", Bd * T3 * (nt - j - 1), Bd * 8.0 * TS * TS * (2.0 * (nt - j - 1) + 1.0),
+            [&] { gprx::launch_trsm(db, j, c->stream); });
+  }
+  for (int s = 1; s < db.nt; ++s)
+    timed(c, "trtri", Bd * (2.0 * T3 * s * (nt - s)), Bd * 8.0 * TS * TS * (nt - s) * (2.0 * s + 3.0),
+          [&] { gprx::launch_trtri(db, s, c->stream); });
+  timed(c, "alpha", Bd * Np * Np, Bd * 8.0 * Np * Np / 2.0, [&] { gprx::launch_alpha(db, c->stream, 0); });
+  timed(c, "alpha", Bd * Np * Np, Bd * 8.0 * Np * Np / 2.0, [&] { gprx::launch_alpha(db, c->stream, 1); });
+  const bool want_grad = (flags & GPRX_WANT_GRAD) != 0;
+  if (want_grad)
+    timed(c, "lauum_grad", Bd * (Np * Np * Np / 3.0 + 2.0 * Np * Np * d + 4.0 * Np * Np),
+          Bd * 8.0 * TS * TS * (nt * (nt + 1.0) * (nt + 2.0) / 3.0),
+          [&] { gprx::launch_lauum_grad(db, c->stream); });
+  timed(c, "finalize", Bd * 2.0 * db.N, Bd * 16.0 * db.N, [&] { gprx::launch_finalize(db, want_grad ? 1 : 0, c->stream); });
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(b->h_out, db.out, (size_t)B * (d + 3) * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(b->h_status, db.status, 2 * (size_t)B * sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  const bool want_pred = (flags & GPRX_WANT_PREDICT) != 0 && b->have_test && db.M > 0;
+  if (want_pred) {
+    int rc = run_predict_kernels(b);
+    if (rc) return rc;
+    HIPCHK(c, hipMemcpyAsync(b->h_mu, db.out_mu, (size_t)B * db.Mpad * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(b->h_var, db.out_var, (size_t)B * db.Mpad * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  collect(c);
+  int first = GPRX_OK;
+  for (int s = 0; s < B; ++s) {
+    const int st = b->h_status[s];
+    if (status) status[s] = st;
+    if (info) info[s] = b->h_status[B + s];
+    if (st != GPRX_OK && first == GPRX_OK) first = st;
+    const double* o = b->h_out + (size_t)s * (d + 3);
+    if (mll) mll[s] = o[0];
+    if (grad && want_grad) memcpy(grad + (size_t)s * np, o + 1, np * sizeof(double));
+    if (want_pred) {
+      if (mu) memcpy(mu + (size_t)s * db.M, b->h_mu + (size_t)s * db.Mpad, db.M * sizeof(double));
+      if (var) memcpy(var + (size_t)s * db.M, b->h_var + (size_t)s * db.Mpad, db.M * sizeof(double));
+    }
+  }
+  b->factored = true;
+  if (first != GPRX_OK) set_err(c, first, std::string("gprx_batch_run: ") + gprx_status_string(first));
+  return first;
+}
+
+int gprx_batch_predict(gprx_batch* b, double* mu, double* var) {
+  if (!b) return GPRX_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> g(b->ctx->mu);
+  if (hipSetDevice(b->ctx->device) != hipSuccess) return GPRX_DEVICE_ERROR;
+  return batch_predict_locked(b, mu, var);
+}
+
+// ---- single GP ---------------------------------------------------------------------------------
+int gprx_gp_create(gprx_ctx* c, const double* X, int d, int N, const double* y, gprx_gp** out) {
+  if (!c || !X || !y || !out) return GPRX_INVALID_ARGUMENT;
+  *out = nullptr;
+  gprx_batch* b = nullptr;
+  int rc = gprx_batch_create(c, 1, d, N, 0, &b);
+  if (rc) return rc;
+  rc = gprx_batch_set_train(b, X, 0, y, 0, GPRX_MEM_HOST);
+  if (rc) {
+    gprx_batch_destroy(b);
+    return rc;
+  }
+  gprx_gp* gp = new gprx_gp();
+  gp->batch = b;
+  *out = gp;
+  return GPRX_OK;
+}
+
+void gprx_gp_destroy(gprx_gp* gp) {
+  if (!gp) return;
+  gprx_batch_destroy(gp->batch);
+  delete gp;
+}
+
+int gprx_gp_lml(gprx_gp* gp, const double* theta, double* mll) {
+  if (!gp) return GPRX_INVALID_ARGUMENT;
+  return gprx_batch_run(gp->batch, theta, 0u, mll, nullptr, nullptr, nullptr, nullptr, nullptr);
+}
+
+int gprx_gp_lml_grad(gprx_gp* gp, const double* theta, double* mll, double* grad) {
+  if (!gp) return GPRX_INVALID_ARGUMENT;
+  return gprx_batch_run(gp->batch, theta, GPRX_WANT_GRAD, mll, grad, nullptr, nullptr, nullptr, nullptr);
+}
+
+int gprx_gp_predict(gprx_gp* gp, const double* Xs, int M, double* mu, double* var) {
+  if (!gp || M < 0) return GPRX_INVALID_ARGUMENT;
+  if (M == 0) return GPRX_OK;
+  int rc = gprx_batch_set_test(gp->batch, Xs, M, 0, GPRX_MEM_HOST);
+  if (rc) return rc;
+  return gprx_batch_predict(gp->batch, mu, var);
+}
+
+// ---- host CState helpers -----------------------------------------------------------------------
+int gprx_cstate_pack(int nb, const double* xc, const double* q, const double* vc, const double* wc, double* out) {
+  if (nb < 1 || !xc || !q || !vc || !wc || !out) return GPRX_INVALID_ARGUMENT;
+  for (int b = 0; b < nb; ++b) {
+    double* o = out + 13 * b;
+    for (int k = 0; k < 3; ++k) o[k] = xc[3 * b + k];
+    for (int k = 0; k < 4; ++k) o[3 + k] = q[4 * b + k];
+    for (int k = 0; k < 3; ++k) o[7 + k] = vc[3 * b + k];
+    for (int k = 0; k < 3; ++k) o[10 + k] = wc[3 * b + k];
+  }
+  return GPRX_OK;
+}
+
+int gprx_select_outputs(const double* Xc, int d, int N, const int* idx1, int G, double* Y) {
+  if (!Xc || !idx1 || !Y || d < 1 || N < 0 || G < 0) return GPRX_INVALID_ARGUMENT;
+  for (int k = 0; k < G; ++k)
+    if (idx1[k] < 1 || idx1[k] > d) return GPRX_INVALID_ARGUMENT;
+  for (int k = 0; k < G; ++k)
+    for (int t = 0; t < N; ++t) Y[(size_t)k * N + t] = Xc[(size_t)t * d + (idx1[k] - 1)];
+  return GPRX_OK;
+}
+
+}  // extern "C"

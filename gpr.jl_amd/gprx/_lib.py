@@ -1,0 +1,109 @@
+"""ctypes binding of the C ABI declared in include/gprx.h (libgprx.so, built for gfx950).
+
+There is no CPU fallback: if the shared library is missing this module raises at import time, and
+every compute entry point runs on the MI355X through the library.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import pathlib
+
+_HERE = pathlib.Path(__file__).resolve().parent
+LIB_PATH = pathlib.Path(os.environ.get("GPRX_LIB", _HERE.parent / "lib" / "libgprx.so"))
+
+OK = 0
+NOT_POSITIVE_DEFINITE = 1
+INVALID_ARGUMENT = 2
+DEVICE_ERROR = 3
+OUT_OF_MEMORY = 4
+NOT_READY = 5
+
+WANT_GRAD = 1
+WANT_PREDICT = 2
+
+DIST_EXPANDED = 0
+DIST_DIRECT = 1
+
+MEM_HOST = 0
+MEM_DEVICE = 1
+
+_dp = C.POINTER(C.c_double)
+_ip = C.POINTER(C.c_int)
+_vp = C.c_void_p
+
+# name -> (restype, argtypes); must list every function declared in include/gprx.h
+SIGNATURES = {
+    "gprx_abi_version": (C.c_int, []),
+    "gprx_status_string": (C.c_char_p, [C.c_int]),
+    "gprx_ctx_create": (C.c_int, [C.c_int, C.POINTER(_vp)]),
+    "gprx_ctx_destroy": (None, [_vp]),
+    "gprx_ctx_last_error": (C.c_char_p, [_vp]),
+    "gprx_ctx_set_dist_mode": (C.c_int, [_vp, C.c_int]),
+    "gprx_ctx_device": (C.c_int, [_vp]),
+    "gprx_ctx_set_profiling": (C.c_int, [_vp, C.c_int]),
+    "gprx_ctx_kernel_stats": (C.c_int, [_vp, C.c_char_p, _dp, C.POINTER(C.c_int64), _dp, _dp]),
+    "gprx_ctx_reset_stats": (C.c_int, [_vp]),
+    "gprx_batch_create": (C.c_int, [_vp, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(_vp)]),
+    "gprx_batch_destroy": (None, [_vp]),
+    "gprx_batch_set_train": (C.c_int, [_vp, _vp, C.c_int64, _vp, C.c_int64, C.c_int]),
+    "gprx_batch_set_test": (C.c_int, [_vp, _vp, C.c_int, C.c_int64, C.c_int]),
+    "gprx_batch_run": (C.c_int, [_vp, _dp, C.c_uint, _dp, _dp, _dp, _dp, _ip, _ip]),
+    "gprx_batch_predict": (C.c_int, [_vp, _dp, _dp]),
+    "gprx_batch_dims": (C.c_int, [_vp, _ip, _ip, _ip, _ip]),
+    "gprx_gp_create": (C.c_int, [_vp, _dp, C.c_int, C.c_int, _dp, C.POINTER(_vp)]),
+    "gprx_gp_destroy": (None, [_vp]),
+    "gprx_gp_lml": (C.c_int, [_vp, _dp, _dp]),
+    "gprx_gp_lml_grad": (C.c_int, [_vp, _dp, _dp, _dp]),
+    "gprx_gp_predict": (C.c_int, [_vp, _dp, C.c_int, _dp, _dp]),
+    "gprx_cstate_pack": (C.c_int, [C.c_int, _dp, _dp, _dp, _dp, _dp]),
+    "gprx_select_outputs": (C.c_int, [_dp, C.c_int, C.c_int, _ip, C.c_int, _dp]),
+}
+
+
+def _load():
+    if not LIB_PATH.exists():
+        raise ImportError(
+            f"gprx: native library {LIB_PATH} not found -- build it with "
+            "`make -C gpr.jl_amd` (or __graft_entry__.build()); there is no CPU fallback"
+        )
+    lib = C.CDLL(str(LIB_PATH))
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+class GPRXError(RuntimeError):
+    def __init__(self, status: int, msg: str = ""):
+        s = lib.gprx_status_string(status).decode()
+        super().__init__(f"gprx status {status} ({s}){': ' + msg if msg else ''}")
+        self.status = status
+
+
+class NotPositiveDefinite(GPRXError):
+    """Mirrors LinearAlgebra.PosDefException raised by cholesky! in the reference [ext]."""
+
+
+def check(status: int, ctx=None):
+    if status == OK:
+        return
+    msg = ""
+    if ctx is not None:
+        m = lib.gprx_ctx_last_error(ctx)
+        msg = m.decode() if m else ""
+    if status == NOT_POSITIVE_DEFINITE:
+        raise NotPositiveDefinite(status, msg)
+    raise GPRXError(status, msg)
+
+
+def dptr(a):
+    return a.ctypes.data_as(_dp) if a is not None else None
+
+
+def iptr(a):
+    return a.ctypes.data_as(_ip) if a is not None else None

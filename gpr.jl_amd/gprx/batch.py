@@ -1,0 +1,168 @@
+"""Context / batch wrappers over the C ABI (include/gprx.h).
+
+A `GPBatch` holds B GP slots of equal (d, N) in HBM -- the G per-output GPs of a trial
+(examples/maximal_coordinates/CPnoise.jl:37-43) and/or several trials (examples/parallel/core.jl:28)
+-- and evaluates all of them with one launch sequence per call.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import threading
+
+import numpy as np
+
+from . import _lib as L
+
+_ctx_lock = threading.Lock()
+_default_ctx: dict[int, "Context"] = {}
+
+
+class Context:
+    """One device + one HIP stream (gprx_ctx).  Safe to share across threads; calls serialise."""
+
+    def __init__(self, device: int = 0, dist_mode: int = L.DIST_EXPANDED):
+        h = C.c_void_p()
+        L.check(L.lib.gprx_ctx_create(int(device), C.byref(h)))
+        self.h = h
+        self.device = int(device)
+        self.set_dist_mode(dist_mode)
+
+    def set_dist_mode(self, mode: int):
+        L.check(L.lib.gprx_ctx_set_dist_mode(self.h, int(mode)), self.h)
+        self.dist_mode = int(mode)
+
+    def set_profiling(self, enable: bool):
+        L.check(L.lib.gprx_ctx_set_profiling(self.h, 1 if enable else 0), self.h)
+
+    def reset_stats(self):
+        L.check(L.lib.gprx_ctx_reset_stats(self.h), self.h)
+
+    def kernel_stats(self, name: str) -> dict:
+        ms = C.c_double()
+        n = C.c_int64()
+        fl = C.c_double()
+        by = C.c_double()
+        L.check(L.lib.gprx_ctx_kernel_stats(self.h, name.encode(), C.byref(ms), C.byref(n), C.byref(fl), C.byref(by)))
+        return dict(ms=ms.value, launches=n.value, flops=fl.value, bytes=by.value)
+
+    def close(self):
+        if getattr(self, "h", None):
+            L.lib.gprx_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def default_context(device: int = 0) -> Context:
+    with _ctx_lock:
+        c = _default_ctx.get(device)
+        if c is None:
+            c = Context(device)
+            _default_ctx[device] = c
+        return c
+
+
+def _f64(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+class GPBatch:
+    """B exact SE-ARD GPs with shared (d, N); per-slot X, y, theta.
+
+    X: (B, d, N) or (d, N) shared; y: (B, N) = targets minus prior mean.
+    theta rows: [logσn, logℓ_1..d, logσf] (GaussianProcesses get_params order).
+    """
+
+    def __init__(self, B: int, d: int, N: int, M_max: int = 0, ctx: Context | None = None):
+        self.ctx = ctx or default_context()
+        h = C.c_void_p()
+        L.check(L.lib.gprx_batch_create(self.ctx.h, int(B), int(d), int(N), int(M_max), C.byref(h)), self.ctx.h)
+        self.h = h
+        self.B, self.d, self.N = int(B), int(d), int(N)
+        self.M = 0
+
+    # -- inputs -----------------------------------------------------------------------------
+    def set_train(self, X, Y):
+        """Host numpy arrays.  X: (d, N) shared or (B, d, N); Y: (B, N)."""
+        X = _f64(X)
+        Y = _f64(Y)
+        if X.ndim == 2:
+            assert X.shape == (self.d, self.N), X.shape
+            xs = 0
+        else:
+            assert X.shape == (self.B, self.d, self.N), X.shape
+            xs = self.d * self.N
+        assert Y.shape == (self.B, self.N), Y.shape
+        # numpy (d, N) row-major is the transpose of the ABI's d x N column-major layout
+        Xc = np.ascontiguousarray(np.swapaxes(X, -1, -2))  # (..., N, d): column t contiguous
+        L.check(L.lib.gprx_batch_set_train(self.h, Xc.ctypes.data, xs, Y.ctypes.data, self.N, L.MEM_HOST), self.ctx.h)
+
+    def set_train_device(self, X_ptr: int, x_slot_stride: int, Y_ptr: int, y_slot_stride: int):
+        """Device pointers (e.g. torch tensors' data_ptr()), ABI layout: per slot N x d row-major
+        (= d x N column-major) and N targets."""
+        L.check(
+            L.lib.gprx_batch_set_train(self.h, C.c_void_p(X_ptr), x_slot_stride, C.c_void_p(Y_ptr), y_slot_stride,
+                                       L.MEM_DEVICE),
+            self.ctx.h,
+        )
+
+    def set_test(self, Xs):
+        """Xs: (d, M) shared or (B, d, M)."""
+        Xs = _f64(Xs)
+        if Xs.ndim == 2:
+            M = Xs.shape[1]
+            xs = 0
+        else:
+            assert Xs.shape[0] == self.B
+            M = Xs.shape[2]
+            xs = self.d * M
+        assert Xs.shape[-2] == self.d
+        Xc = np.ascontiguousarray(np.swapaxes(Xs, -1, -2))
+        L.check(L.lib.gprx_batch_set_test(self.h, Xc.ctypes.data, int(M), xs, L.MEM_HOST), self.ctx.h)
+        self.M = int(M)
+
+    def set_test_device(self, Xs_ptr: int, M: int, xs_slot_stride: int):
+        L.check(L.lib.gprx_batch_set_test(self.h, C.c_void_p(Xs_ptr), int(M), xs_slot_stride, L.MEM_DEVICE), self.ctx.h)
+        self.M = int(M)
+
+    # -- evaluation ---------------------------------------------------------------------------
+    def run(self, theta, grad: bool = True, predict: bool = False, raise_on_error: bool = False):
+        """Returns dict(mll[B], grad[B,d+2] | None, mu[B,M] | None, var[B,M] | None, status[B], info[B])."""
+        theta = _f64(theta)
+        if theta.ndim == 1:
+            theta = np.broadcast_to(theta, (self.B, self.d + 2)).copy()
+        assert theta.shape == (self.B, self.d + 2), theta.shape
+        mll = np.empty(self.B)
+        g = np.empty((self.B, self.d + 2)) if grad else None
+        pred = predict and self.M > 0
+        mu = np.empty((self.B, self.M)) if pred else None
+        var = np.empty((self.B, self.M)) if pred else None
+        st = np.empty(self.B, dtype=np.int32)
+        info = np.empty(self.B, dtype=np.int32)
+        flags = (L.WANT_GRAD if grad else 0) | (L.WANT_PREDICT if pred else 0)
+        rc = L.lib.gprx_batch_run(self.h, L.dptr(theta), flags, L.dptr(mll), L.dptr(g), L.dptr(mu), L.dptr(var),
+                                  L.iptr(st), L.iptr(info))
+        if rc not in (L.OK, L.NOT_POSITIVE_DEFINITE, L.INVALID_ARGUMENT) or (raise_on_error and rc != L.OK):
+            L.check(rc, self.ctx.h)
+        return dict(mll=mll, grad=g, mu=mu, var=var, status=st, info=info)
+
+    def predict(self):
+        mu = np.empty((self.B, self.M))
+        var = np.empty((self.B, self.M))
+        L.check(L.lib.gprx_batch_predict(self.h, L.dptr(mu), L.dptr(var)), self.ctx.h)
+        return mu, var
+
+    def close(self):
+        if getattr(self, "h", None):
+            L.lib.gprx_batch_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,125 @@
+/*
+ * gprx.h -- C ABI of the MI355X-native exact-GP (SE-ARD, fp64) hot path for GPR.jl.
+ *
+ * Plain C: pointers, sizes, status codes.  No torch / HIP types cross this boundary.
+ *
+ * What each entry point replaces in the reference (amacati/GPR.jl, whose GP arithmetic is
+ * delegated to GaussianProcesses.jl v0.12.4, pinned in /root/reference/Manifest.toml):
+ *
+ *   gprx_gp_create / gprx_batch_set_train
+ *       GP(xtrain_old, yi, mean, kernel)            examples/maximal_coordinates/CPnoise.jl:40
+ *       (X = reduce(hcat, CState.(traindf.sold)),   CPnoise.jl:26; y = yi - mean(X),
+ *        mean from MeanZero or MeanDynamics         src/mDynamics.jl:41-55, theta-independent :29)
+ *   gprx_gp_lml        update_mll! inside GP()/optimize! value evaluations   [ext] CPnoise.jl:40-41
+ *   gprx_gp_lml_grad   update_mll! + update_dmll! (one LBFGS evaluation)     [ext] CPnoise.jl:41
+ *   gprx_gp_predict    predict_f / predict_y(gp, x*)  examples/utils/predictdynamics.jl:13
+ *   gprx_batch_*       the G per-output GPs of a trial (CPnoise.jl:37-43) and the trial loop
+ *                      (examples/parallel/core.jl:28) evaluated as one device batch
+ *   gprx_cstate_pack   CState(::Vector{State})      src/CState.jl:25-28
+ *   gprx_select_outputs  ytrain = [[s[i] for s in X_curr] for i in vwindices]   CPnoise.jl:28-29
+ *
+ * Hyper-parameter vector convention (GaussianProcesses get_params(gp) order, d+2 entries):
+ *     theta = [ log sigma_n, log ell_1 ... log ell_d, log sigma_f ]
+ * built by the callers as SEArd(log.(p[2:end]), log(p[1])) with default logNoise = -2.0
+ * (CPnoise.jl:38-40).  Gradients are returned in the same order, with the same sign as
+ * GaussianProcesses' gp.dmll (derivative of the log marginal likelihood, not of -mll).
+ *
+ * Memory: the caller owns every buffer it passes; the library copies on entry.  A batch owns
+ * its device workspace (X, y, K/L, L^-1, L^-T, alpha, test points) until destroyed.
+ * Threading: a context owns one HIP stream and a mutex; calls on one context serialise, calls on
+ * different contexts (e.g. one per Julia thread / per GPU) run concurrently.  All calls block
+ * until results are in host memory.
+ */
+#ifndef GPRX_H
+#define GPRX_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GPRX_ABI_VERSION 1
+
+/* status codes (mirrors the reference's failure modes) */
+#define GPRX_OK 0
+#define GPRX_NOT_POSITIVE_DEFINITE 1 /* cholesky! -> PosDefException; Optim then sees +Inf   */
+#define GPRX_INVALID_ARGUMENT 2      /* bad sizes, non-finite theta (ArgumentError)          */
+#define GPRX_DEVICE_ERROR 3
+#define GPRX_OUT_OF_MEMORY 4
+#define GPRX_NOT_READY 5 /* predict before any successful factorisation */
+
+/* gprx_batch_run flags */
+#define GPRX_WANT_GRAD 1u    /* d mll / d theta (update_dmll!)                          */
+#define GPRX_WANT_PREDICT 2u /* predictive mean + variance at the batch's test points    */
+
+/* squared-distance formulation of the SE-ARD kernel (see DESIGN.md "distance modes") */
+#define GPRX_DIST_EXPANDED 0 /* Distances.jl 0.10.5 pairwise SqEuclidean: a^2 + b^2 - 2ab (default) */
+#define GPRX_DIST_DIRECT 1   /* (a - b)^2                                                            */
+
+/* memory kind of pointer arguments */
+#define GPRX_MEM_HOST 0
+#define GPRX_MEM_DEVICE 1
+
+typedef struct gprx_ctx gprx_ctx;
+typedef struct gprx_batch gprx_batch;
+typedef struct gprx_gp gprx_gp;
+
+int gprx_abi_version(void);
+const char* gprx_status_string(int status);
+
+/* ---- context: one device, one stream ------------------------------------------------------ */
+int gprx_ctx_create(int device, gprx_ctx** out);
+void gprx_ctx_destroy(gprx_ctx* ctx);
+const char* gprx_ctx_last_error(const gprx_ctx* ctx);
+int gprx_ctx_set_dist_mode(gprx_ctx* ctx, int mode);
+int gprx_ctx_device(const gprx_ctx* ctx);
+/* per-kernel timing (HIP events around every launch on the context stream); off by default */
+int gprx_ctx_set_profiling(gprx_ctx* ctx, int enable);
+int gprx_ctx_kernel_stats(gprx_ctx* ctx, const char* kernel, double* total_ms, int64_t* launches,
+                          double* algo_flops, double* algo_bytes);
+int gprx_ctx_reset_stats(gprx_ctx* ctx);
+
+/* ---- batch: B GP slots with equal (d, N); slot b has its own X_b, y_b, theta_b ------------ */
+/* M_max: maximum number of test points per slot (0 = no prediction).  d <= 64, N >= 1.        */
+int gprx_batch_create(gprx_ctx* ctx, int B, int d, int N, int M_max, gprx_batch** out);
+void gprx_batch_destroy(gprx_batch* batch);
+/* X: d x N column-major per slot (column t = one CState), slot b at X + b*x_slot_stride
+ *    (x_slot_stride = 0: all slots share one X, as the G outputs of one trial do);
+ * Y: N targets per slot (y - mean(X)), slot b at Y + b*y_slot_stride.                          */
+int gprx_batch_set_train(gprx_batch* batch, const double* X, int64_t x_slot_stride, const double* Y,
+                         int64_t y_slot_stride, int mem);
+/* Xs: d x M column-major per slot, slot b at Xs + b*xs_slot_stride (0 = shared), M <= M_max.   */
+int gprx_batch_set_test(gprx_batch* batch, const double* Xs, int M, int64_t xs_slot_stride, int mem);
+/* Evaluate every slot at theta[b*(d+2) ...]: Gram build, Cholesky, alpha, log marginal
+ * likelihood; optionally its gradient and the predictive mean/variance (f-space: no noise, no
+ * prior mean) at the test points.  Outputs (host pointers, any may be NULL):
+ *   mll[B], grad[B*(d+2)], mu[B*M], var[B*M], status[B], info[B] (1-based failing pivot).
+ * Returns GPRX_OK when every slot succeeded, otherwise the first failing slot's status.          */
+int gprx_batch_run(gprx_batch* batch, const double* theta, unsigned flags, double* mll, double* grad,
+                   double* mu, double* var, int* status, int* info);
+/* Predictive mean/variance from the factorisation of the last gprx_batch_run (f-space).       */
+int gprx_batch_predict(gprx_batch* batch, double* mu, double* var);
+int gprx_batch_dims(const gprx_batch* batch, int* B, int* d, int* N, int* M_max);
+
+/* ---- single GP: the GPE surface, a batch of one ------------------------------------------- */
+int gprx_gp_create(gprx_ctx* ctx, const double* X, int d, int N, const double* y_minus_mean,
+                   gprx_gp** out);
+void gprx_gp_destroy(gprx_gp* gp);
+int gprx_gp_lml(gprx_gp* gp, const double* theta, double* mll);
+int gprx_gp_lml_grad(gprx_gp* gp, const double* theta, double* mll, double* grad);
+/* f-space predictive mean (k*^T alpha) and variance (max(k** - |L^-1 k*|^2, 0)) at the
+ * factorisation of the last lml call; var may be NULL.                                          */
+int gprx_gp_predict(gprx_gp* gp, const double* Xs, int M, double* mu_f, double* var_f);
+
+/* ---- host-side CState helpers (bit-exact copies) ------------------------------------------ */
+/* out[13*b + 0..12] = [xc(3), qc.w, qc.x, qc.y, qc.z, vc(3), wc(3)] for body b (CState.jl:20,26) */
+int gprx_cstate_pack(int nbodies, const double* xc, const double* qc_wxyz, const double* vc,
+                     const double* wc, double* out);
+/* Y[k*N + t] = Xcurr[t*d + (idx1[k]-1)]  (1-based indices, as vwindices in the experiments)     */
+int gprx_select_outputs(const double* Xcurr, int d, int N, const int* idx1, int G, double* Y);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GPRX_H */
