@@ -1,0 +1,198 @@
+#!/usr/bin/env python3
+"""GP fits/sec on MI355X (BASELINE.json metric), fp64, N=2048, d=26 CState (P2 double pendulum).
+
+One "fit"  = Gram build + Cholesky + alpha + log marginal likelihood,
+one full gradient of the LML (one optimiser evaluation), and the predictive mean + variance at
+M=100 test CStates -- for one per-output GP at its own hyper-parameters.
+One "step" = one batch of fits: T trials x 6 output GPs (vwindices of P2noise.jl:25) per GPU,
+each GP with its own theta (config.json P2_MAX2048 jittered, as during optimisation), inputs
+resident in HBM before the timed region.
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N>1 under torch.distributed.run
+(one rank per GPU).  Trials are sharded over ranks (weak scaling, no data-path collective).
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import pathlib
+import sys
+import time
+
+import numpy as np
+
+REPO = pathlib.Path(__file__).resolve().parent
+sys.path.insert(0, str(REPO / "gpr.jl_amd"))
+
+MECH, N, M, KEY = "P2", 2048, 100, 2048
+G = 6
+PEAK_FP64_TFLOPS = 78.6  # MI355X fp64 matrix (measured 77.6 with back-to-back v_mfma_f64_16x16x4)
+PEAK_HBM_GBS = 8000.0
+
+
+def fit_flops(N: int, d: int, Mt: int) -> float:
+    """Algorithmic flops of one fit, SURVEY.md section 8d."""
+    return (3 * N * N * d + N**3 / 3 + 2 * N * N + 2 * N**3 / 3 + 2 * N * N * d + 4 * N * N
+            + N * N * Mt + 3 * N * Mt * d + 2 * N * Mt)
+
+
+def make_workload(trials_per_gpu: int, rank: int, world: int, seed_base: int = 0):
+    from gprx import data
+
+    th0 = data.theta0(MECH, KEY)
+    Xs, Ys, Ts, XTs = [], [], [], []
+    for k in range(trials_per_gpu):
+        trial = rank + world * k  # trial-major round robin over ranks
+        tr = data.make_trial(MECH, N, M, seed=data.trial_seed(MECH, trial) + seed_base)
+        rng = np.random.default_rng(10_000 + trial)
+        for g in range(G):
+            Xs.append(tr["X"])
+            XTs.append(tr["Xs"])
+            Ys.append(tr["Y"][g])
+            Ts.append(th0 + 0.05 * rng.standard_normal(th0.shape[0]))
+    return np.stack(Xs), np.stack(Ys), np.stack(Ts), np.stack(XTs)
+
+
+def cpu_baseline(X, Y, T, XT, max_seconds: float = 20.0, max_fits: int = 3):
+    """Oracle (CPU restatement, numpy + OpenBLAS LAPACK) on a bounded sample of the same workload."""
+    sys.path.insert(0, str(REPO))
+    from oracle import gp_oracle as O
+
+    try:
+        from threadpoolctl import threadpool_info
+
+        threads = max([i.get("num_threads", 1) for i in threadpool_info() if i.get("internal_api") == "openblas"] or [1])
+    except Exception:
+        threads = int(os.environ.get("OMP_NUM_THREADS", "1"))
+    t0 = time.perf_counter()
+    n = 0
+    for s in range(min(max_fits, X.shape[0])):
+        O.fit(X[s], Y[s], T[s], XT[s])
+        n += 1
+        if time.perf_counter() - t0 > max_seconds:
+            break
+    dt = time.perf_counter() - t0
+    return dict(value=n / dt, unit="fits/s", cores=int(threads), kind="port",
+                sample=f"{n} P2 fits (N=2048, d=26, M=100) via oracle/gp_oracle.py: reference algorithm "
+                       f"(Distances-style dist stack, OpenBLAS dpotrf, K^-1 by cho_solve(I), per-param grad "
+                       f"sums), {dt:.1f}s, OpenBLAS threads={threads}")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--trials", type=int, default=int(os.environ.get("GPRX_BENCH_TRIALS", "8")),
+                    help="P2 trials per GPU per step (x6 output GPs)")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-prof", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    else:
+        torch.cuda.set_device(local)
+
+    import gprx
+
+    ctx = gprx.Context(local)
+    X, Y, T, XT = make_workload(args.trials, rank, world)
+    B, d = X.shape[0], X.shape[1]
+    batch = gprx.GPBatch(B, d, N, M, ctx=ctx)
+    batch.set_train(X, Y)
+    batch.set_test(XT)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        r = batch.run(T, grad=True, predict=True)
+    ok = bool(np.all(r["status"] == 0)) if args.warmup else True
+
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        r = batch.run(T, grad=True, predict=True)
+    barrier()
+    dt = time.perf_counter() - t0
+    ok = ok and bool(np.all(r["status"] == 0))
+    if dist is not None:
+        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    fits = B * args.steps * world
+    value = fits / dt
+
+    # roofline: per-kernel HIP-event timing on the library stream, same workload, separate pass
+    roof = None
+    kern = {}
+    if not args.no_prof:
+        ctx.set_profiling(True)
+        ctx.reset_stats()
+        nprof = max(1, min(args.steps, 3))
+        for _ in range(nprof):
+            batch.run(T, grad=True, predict=True)
+        ctx.set_profiling(False)
+        names = ["gram", "potrf_update", "potrf_diag", "trsm", "trtri", "alpha", "lauum_grad", "finalize",
+                 "pred_cross", "pred_var", "pred_final"]
+        for nme in names:
+            kern[nme] = ctx.kernel_stats(nme)
+        dom = max(kern, key=lambda k: kern[k]["ms"])
+        s = kern[dom]
+        avg_ms = s["ms"] / max(1, s["launches"])
+        per_launch_flops = s["flops"] / max(1, s["launches"])
+        achieved = per_launch_flops / (avg_ms * 1e-3) / 1e12
+        roof = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 3), "peak": PEAK_FP64_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP64_TFLOPS, 4), "traffic": None,
+                "avg_launch_ms": round(avg_ms, 4), "launches_per_step": s["launches"] // nprof}
+    step_flops = B * fit_flops(N, d, M)
+    cpu = None
+    if rank == 0 and not args.no_cpu:
+        cpu = cpu_baseline(X, Y, T, XT)
+
+    if rank == 0:
+        out = {
+            "metric": "GP fits/sec (fp64, N=2048, d=26 CState)",
+            "value": round(value, 3),
+            "unit": "fits/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (P2 CState generator, reference kinematics; theta from config.json P2_MAX2048)",
+            "config": {"workload": f"P2 double pendulum: {args.trials} trials x {G} output GPs per GPU, N={N}, "
+                                   f"d={d}, M={M} test points; fit = Gram+Cholesky+alpha+LML, full dLML, predict mean+var",
+                       "global_batch": fits // args.steps, "N": N, "d": d, "M": M, "parallelism": f"trial-shard x{world}"},
+            "fit_ok": ok,
+            "whole_step_tflops": round(step_flops / (dt / args.steps) / 1e12 * 1.0, 3),
+            "whole_step_frac_of_fp64_peak": round(step_flops / (dt / args.steps) / 1e12 / PEAK_FP64_TFLOPS, 4),
+            "roofline": roof,
+            "kernels_ms_per_step": {k: round(v["ms"] / max(1, (min(args.steps, 3))), 3) for k, v in kern.items()} if kern else None,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
