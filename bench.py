@@ -147,8 +147,8 @@ def main():
         for _ in range(nprof):
             batch.run(T, grad=True, predict=True)
         ctx.set_profiling(False)
-        names = ["gram", "potrf_update", "potrf_diag", "trsm", "trtri", "alpha", "lauum_grad", "finalize",
-                 "pred_cross", "pred_var", "pred_final"]
+        names = ["gram", "diag", "potrf_trsm", "potrf_syrk", "trtri_tt", "trtri_linv21", "alpha", "lauum_grad",
+                 "finalize", "pred_cross", "pred_var", "pred_final"]
         for nme in names:
             kern[nme] = ctx.kernel_stats(nme)
         dom = max(kern, key=lambda k: kern[k]["ms"])

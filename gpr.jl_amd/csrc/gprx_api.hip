@@ -178,14 +178,41 @@ int copy_in(gprx_ctx* c, void* dst, const void* src, size_t bytes, int mem) {
   return GPRX_OK;
 }
 
+// Recursive Cholesky + inverse over tile range [o, o+n) (tile units), all slots in lock step.
+void factor_rec(gprx_ctx* c, const DevBatch& db, int o, int n) {
+  const double T = TS, Bd = db.B;
+  if (n == 1) {
+    timed(c, "diag", Bd * (T * T * T / 3.0 + T * T * T / 3.0), Bd * 8.0 * 3.0 * T * T,
+          [&] { gprx::launch_diag(db, o, c->stream); });
+    return;
+  }
+  const int h = n / 2;
+  const double m1 = h * T, m2 = (n - h) * T;
+  factor_rec(c, db, o, h);
+  gprx::GemmGeom g{gprx::OP_TRSM, o, h, n};
+  timed(c, "potrf_trsm", Bd * m2 * m1 * m1, Bd * 8.0 * (2.0 * m2 * m1 + m1 * m1 / 2.0),
+        [&] { gprx::launch_gemm(db, g, c->stream); });
+  g.op = gprx::OP_SYRK;
+  timed(c, "potrf_syrk", Bd * m2 * m2 * m1, Bd * 8.0 * (m2 * m1 + m2 * m2),
+        [&] { gprx::launch_gemm(db, g, c->stream); });
+  factor_rec(c, db, o + h, n - h);
+  g.op = gprx::OP_TT;
+  timed(c, "trtri_tt", Bd * m2 * m1 * m1, Bd * 8.0 * (2.0 * m2 * m1 + m1 * m1 / 2.0),
+        [&] { gprx::launch_gemm(db, g, c->stream); });
+  g.op = gprx::OP_LINV21;
+  timed(c, "trtri_linv21", Bd * m1 * m2 * m2, Bd * 8.0 * (3.0 * m2 * m1 + m2 * m2 / 2.0),
+        [&] { gprx::launch_gemm(db, g, c->stream); });
+}
+
 int run_predict_kernels(gprx_batch* b) {
   gprx_ctx* c = b->ctx;
   const DevBatch& db = b->db;
   const double N = db.N, M = db.M, d = db.d, B = db.B;
   timed(c, "pred_cross", B * (3.0 * N * M * d + 2.0 * N * M), B * 8.0 * (N * db.Mpad + (N + M) * d),
         [&] { gprx::launch_pred_cross(db, c->stream); });
+  gprx::GemmGeom g{gprx::OP_PREDVAR, 0, 0, 0};
   timed(c, "pred_var", B * N * N * M, B * 8.0 * (N * N / 2 + N * db.Mpad),
-        [&] { gprx::launch_pred_var(db, c->stream); });
+        [&] { gprx::launch_gemm(db, g, c->stream); });
   timed(c, "pred_final", B * 2.0 * db.nt * db.Mpad, B * 16.0 * db.nt * db.Mpad,
         [&] { gprx::launch_pred_final(db, c->stream); });
   return GPRX_OK;
@@ -296,6 +323,7 @@ int gprx_batch_create(gprx_ctx* c, int B, int d, int N, int M_max, gprx_batch** 
   db.mat = (size_t)db.Npad * db.Npad;
   db.pst = d + 4;
   db.gps = d + 2;
+  db.ngu = gprx::lauum_units(db.nt);
   const size_t Bs = B;
   int rc = GPRX_OK;
   auto fail = [&](int r) {
@@ -305,13 +333,15 @@ int gprx_batch_create(gprx_ctx* c, int B, int d, int N, int M_max, gprx_batch** 
   if ((rc = dalloc(b, &db.X, Bs * db.Npad * d))) return fail(rc);
   if ((rc = dalloc(b, &db.Y, Bs * db.Npad))) return fail(rc);
   if ((rc = dalloc(b, &db.K, Bs * db.mat))) return fail(rc);
+  if ((rc = dalloc(b, &db.KF, Bs * db.mat))) return fail(rc);
+  if ((rc = dalloc(b, &db.Lw, Bs * db.mat))) return fail(rc);
   if ((rc = dalloc(b, &db.Linv, Bs * db.mat))) return fail(rc);
   if ((rc = dalloc(b, &db.Mt, Bs * db.mat))) return fail(rc);
   if ((rc = dalloc(b, &db.z, Bs * db.Npad))) return fail(rc);
   if ((rc = dalloc(b, &db.alpha, Bs * db.Npad))) return fail(rc);
   if ((rc = dalloc(b, &db.params, Bs * db.pst))) return fail(rc);
   if ((rc = dalloc(b, &db.logdet_part, Bs * db.nt))) return fail(rc);
-  if ((rc = dalloc(b, &db.grad_part, Bs * db.ntl * db.gps))) return fail(rc);
+  if ((rc = dalloc(b, &db.grad_part, Bs * db.ngu * db.gps))) return fail(rc);
   if ((rc = dalloc(b, &db.out, Bs * (d + 3)))) return fail(rc);
   if ((rc = dalloc(b, &db.status, 2 * Bs))) return fail(rc);
   db.info = db.status + Bs;
@@ -322,7 +352,10 @@ int gprx_batch_create(gprx_ctx* c, int B, int d, int N, int M_max, gprx_batch** 
     return fail(set_err(c, GPRX_OUT_OF_MEMORY, "hipHostMalloc failed"));
   // zero padding of X / Y (pad columns never enter a result; kept finite)
   if (hipMemset(db.X, 0, Bs * db.Npad * d * sizeof(double)) != hipSuccess ||
-      hipMemset(db.Y, 0, Bs * db.Npad * sizeof(double)) != hipSuccess)
+      hipMemset(db.Y, 0, Bs * db.Npad * sizeof(double)) != hipSuccess ||
+      hipMemset(db.Lw, 0, Bs * db.mat * sizeof(double)) != hipSuccess ||
+      hipMemset(db.Linv, 0, Bs * db.mat * sizeof(double)) != hipSuccess ||
+      hipMemset(db.Mt, 0, Bs * db.mat * sizeof(double)) != hipSuccess)
     return fail(GPRX_DEVICE_ERROR);
   *out = b;
   return GPRX_OK;
@@ -438,29 +471,16 @@ int gprx_batch_run(gprx_batch* b, const double* theta, unsigned flags, double* m
   }
   HIPCHK(c, hipMemcpyAsync(db.params, b->h_params, (size_t)B * db.pst * sizeof(double), hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemcpyAsync(db.status, b->h_status, 2 * (size_t)B * sizeof(int), hipMemcpyHostToDevice, c->stream));
-  const double T3 = (double)TS * TS * TS, Bd = B, nt = db.nt, Np = db.Npad;
-  timed(c, "gram", Bd * 3.0 * db.N * (double)db.N * d / 2.0, Bd * 8.0 * (Np * Np / 2.0 + Np * d),
+  const double Bd = B, nt = db.nt, Np = db.Npad;
+  timed(c, "gram", Bd * 3.0 * db.N * (double)db.N * d / 2.0, Bd * 8.0 * (Np * Np + Np * d),
         [&] { gprx::launch_gram(db, c->stream); });
-  for (int j = 0; j < db.nt; ++j) {
-    if (j > 0)
-      timed(c, "potrf_update", Bd * (2.0 * T3 * j * (nt - j) - T3 * j),
-            Bd * 8.0 * TS * TS * (2.0 * (nt - j) + j * (nt - j + 1.0)),
-            [&] { gprx::launch_potrf_update(db, j, c->stream); });
-    timed(c, "potrf_diag", Bd * (T3 / 3.0 + T3 / 3.0), Bd * 8.0 * TS * TS * 4.0,
-          [&] { gprx::launch_potrf_diag(db, j, c->stream); });
-    if (j < db.nt - 1)
-      timed(c, "trsm", Bd * T3 * (nt - j - 1), Bd * 8.0 * TS * TS * (2.0 * (nt - j - 1) + 1.0),
-            [&] { gprx::launch_trsm(db, j, c->stream); });
-  }
-  for (int s = 1; s < db.nt; ++s)
-    timed(c, "trtri", Bd * (2.0 * T3 * s * (nt - s)), Bd * 8.0 * TS * TS * (nt - s) * (2.0 * s + 3.0),
-          [&] { gprx::launch_trtri(db, s, c->stream); });
+  factor_rec(c, db, 0, db.nt);
   timed(c, "alpha", Bd * Np * Np, Bd * 8.0 * Np * Np / 2.0, [&] { gprx::launch_alpha(db, c->stream, 0); });
   timed(c, "alpha", Bd * Np * Np, Bd * 8.0 * Np * Np / 2.0, [&] { gprx::launch_alpha(db, c->stream, 1); });
   const bool want_grad = (flags & GPRX_WANT_GRAD) != 0;
   if (want_grad)
     timed(c, "lauum_grad", Bd * (Np * Np * Np / 3.0 + 2.0 * Np * Np * d + 4.0 * Np * Np),
-          Bd * 8.0 * TS * TS * (nt * (nt + 1.0) * (nt + 2.0) / 3.0),
+          Bd * 8.0 * (Np * Np / 2.0 + TS * TS * (nt * (nt + 1.0) * (nt + 2.0) / 3.0)),
           [&] { gprx::launch_lauum_grad(db, c->stream); });
   timed(c, "finalize", Bd * 2.0 * db.N, Bd * 16.0 * db.N, [&] { gprx::launch_finalize(db, want_grad ? 1 : 0, c->stream); });
   HIPCHK(c, hipGetLastError());

@@ -13,19 +13,25 @@ constexpr int DMAX = 64;   // largest input dimension d supported (FB: 52)
 
 // Device-resident state of one batch of B GP slots with equal (d, N).  Passed to every kernel by
 // value.  Matrices are column-major with leading dimension ld = Npad (Npad = ceil(N/64)*64).
-//   K    : Gram matrix, overwritten in place by its lower Cholesky factor L (K = L L^T).
-//   Linv : L^{-1} (lower).          Mt : L^{-T} (upper) = Linv^T, kept so that every GEMM reads
-//                                        operands along contiguous columns.
+//   K    : Gram matrix (lower tiles), reduced in place by the recursive Cholesky's SYRK updates.
+//   KF   : noise-free Gram matrix Kf (lower tiles), read back by the gradient.
+//   Lw   : recursion workspace: L21 blocks (strictly lower tiles) and T^T = L11^-1 L21^T blocks
+//          (strictly upper tiles).
+//   Linv : L^{-1} (lower).      Mt : L^{-T} (upper) = Linv^T, so that every GEMM streams operands
+//                                    along contiguous columns.
 struct DevBatch {
   int B, d, N, Npad, nt, ntl;  // nt = Npad/64 tiles per edge, ntl = nt(nt+1)/2 lower tiles
   int M, Mpad, mt;             // test points (per slot), padded to 64, mt = Mpad/64
   int dist_mode;               // GPRX_DIST_EXPANDED / GPRX_DIST_DIRECT
   int pst;                     // stride of params per slot
-  int gps;                     // stride of per-tile gradient partials (d + 2)
+  int gps;                     // stride of per-unit gradient partials (d + 2)
+  int ngu;                     // gradient partial units per slot
   size_t ld, mat;              // ld = Npad, mat = Npad*Npad
   double* X;                   // B x [Npad][d]   (column t = one CState, contiguous d values)
   double* Y;                   // B x Npad        (y - mean(X), zero padded)
   double* K;                   // B x mat
+  double* KF;                  // B x mat
+  double* Lw;                  // B x mat
   double* Linv;                // B x mat
   double* Mt;                  // B x mat
   double* z;                   // B x Npad        z = L^{-1} y
@@ -33,7 +39,7 @@ struct DevBatch {
   double* params;              // B x pst: [0,d) il2 = exp(-2 log ell), d: sf2, d+1: noise diag
                                //          (sn2 + eps), d+2: sn2
   double* logdet_part;         // B x nt          sum_r log L_rr per diagonal tile
-  double* grad_part;           // B x ntl x gps   per lower tile: S_p (d), S_f, trace(W)
+  double* grad_part;           // B x ngu x gps   per lauum unit: S_p (d), S_f, trace(W)
   double* Xs;                  // B x [Mpad][d]   test points
   double* KsT;                 // B x [Npad][Mpad] K*^T (column-major M x N, ld = Mpad)
   double* mu_part;             // B x nt x Mpad
@@ -45,17 +51,29 @@ struct DevBatch {
   int* info;                   // B
 };
 
+// GEMM operations of the recursive factorisation / inverse / prediction (tile units, see
+// gprx_kernels.hip k_gemm):
+enum GemmOp : int {
+  OP_TRSM = 0,    // Lw[b2,b1]  = K[b2,b1] Linv[b1,b1]^T
+  OP_SYRK = 1,    // K[b2,b2]  -= Lw[b2,b1] Lw[b2,b1]^T   (lower tiles)
+  OP_TT = 2,      // Lw[b1,b2]  = Mt[b1,b1] Lw[b2,b1]^T   (= T^T, T = L21 L11^-1)
+  OP_LINV21 = 3,  // Linv[b2,b1] = -Linv[b2,b2] T ; Mt[b1,b2] = Linv[b2,b1]^T
+  OP_PREDVAR = 4  // var_part   = colsum((Linv K*)^2)
+};
+struct GemmGeom {
+  int op;
+  int o, h, n;  // node: offset o, split h, size n (tile units); block1 = [o, o+h), block2 = [o+h, o+n)
+};
+
 // kernel launchers (gprx_kernels.hip); every launcher is asynchronous on `s`
 void launch_gram(const DevBatch& b, hipStream_t s);
-void launch_potrf_update(const DevBatch& b, int j, hipStream_t s);
-void launch_potrf_diag(const DevBatch& b, int j, hipStream_t s);
-void launch_trsm(const DevBatch& b, int j, hipStream_t s);
-void launch_trtri(const DevBatch& b, int sdiag, hipStream_t s);
+void launch_diag(const DevBatch& b, int jt, hipStream_t s);
+void launch_gemm(const DevBatch& b, const GemmGeom& g, hipStream_t s);
 void launch_alpha(const DevBatch& b, hipStream_t s, int phase);
 void launch_lauum_grad(const DevBatch& b, hipStream_t s);
+int lauum_units(int nt);
 void launch_finalize(const DevBatch& b, int want_grad, hipStream_t s);
 void launch_pred_cross(const DevBatch& b, hipStream_t s);
-void launch_pred_var(const DevBatch& b, hipStream_t s);
 void launch_pred_final(const DevBatch& b, hipStream_t s);
 
 }  // namespace gprx

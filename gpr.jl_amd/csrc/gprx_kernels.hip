@@ -2,20 +2,24 @@
 //
 // Algorithm (restating GaussianProcesses.jl v0.12.4 update_cK!/update_mll!/update_dmll!/predict_f
 // as used by examples/maximal_coordinates/*noise.jl; see DESIGN.md for the kernel map):
-//   K     = sf2 * exp(-r/2) + (sn2 + eps) I,  r_ij = sum_p il2_p * dist_p(x_i, x_j)     (gram)
-//   K     = L L^T      left-looking tile Cholesky (update -> diag -> trsm per tile column)
-//   L^-1  tile by tile, one sub-diagonal per launch                                  (trtri)
+//   K, Kf = sf2 * exp(-r/2) (+ (sn2 + eps) I),  r_ij = sum_p il2_p * dist_p(x_i, x_j)  (gram)
+//   recursive Cholesky + triangular inverse on 64x64 tiles (host recursion, gprx_api.hip):
+//     [A11 .; A21 A22]: rec(A11) -> L11, L11^-1 ; L21 = A21 L11^-T (TRSM) ;
+//     A22 -= L21 L21^T (SYRK) ; rec(A22) ; T^T = L11^-T L21^T (TT) ; L21^-1 = -L22^-1 T (LINV21)
+//     leaves: 64x64 Cholesky + inverse in one workgroup (diag)
 //   alpha = L^-T (L^-1 y)                                                            (alpha)
 //   K^-1  = L^-T L^-1 tile by tile, fused with the gradient reduction of
-//           W = alpha alpha^T - K^-1 against dK/dtheta (never written to HBM)        (lauum_grad)
+//           W = alpha alpha^T - K^-1 against dK/dtheta (K^-1 never written to HBM)   (lauum_grad)
 //   mll, dmll                                                                        (finalize)
 //   mu* = k*^T alpha,  var* = max(sf2 - |L^-1 k*|^2, 0)                             (pred_*)
 //
-// Every dense product is a 64x64 output tile per 256-thread workgroup, 4 waves of 32x32, built
-// from v_mfma_f64_16x16x4_f64 with operands streamed straight from L2 (fp64 MFMA is 64 cycles per
-// instruction per SIMD, so a 2x2 register tile per wave already keeps the pipe fed).
-// Workgroup -> (slot, tile) mapping keeps every slot's tiles on one XCD (blocks b, b+8, ... share
-// an XCD), so the panels all tiles of a slot re-read stay in that XCD's L2.
+// Dense products: one wave computes a 64x32 block with v_mfma_f64_16x16x4_f64 (4x2 16x16
+// accumulators), operands streamed straight from L2 one 16-deep stage ahead (fp64 MFMA is 64
+// cycles per instruction per SIMD; a 4x2 register tile needs 0.75 fragment loads per MFMA).  A
+// workgroup = 4 waves = two vertically adjacent 64x64 tiles sharing their B panel.  Each wave has
+// its own K range, so triangular operands are skipped at tile granularity.
+// Workgroup -> (slot, unit) mapping keeps every slot's units on one XCD (blocks b, b+8, ... share
+// an XCD), so the panels of a slot stay in that XCD's L2.
 #include "gprx_internal.h"
 
 namespace gprx {
@@ -26,49 +30,65 @@ __device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
-// blockIdx -> (slot, tile); slots' tiles on one XCD when B % 8 == 0 (speed only, never correctness)
-__device__ __forceinline__ void map_block(int bid, int B, int T, int& slot, int& tile) {
+// blockIdx -> (slot, unit); a slot's units on one XCD when B % 8 == 0 (speed only, never correctness)
+__device__ __forceinline__ void map_block(int bid, int B, int T, int& slot, int& unit) {
   if ((B & 7) == 0) {
     const int x = bid & 7, q = bid >> 3;
     slot = (q / T) * 8 + x;
-    tile = q % T;
+    unit = q % T;
   } else {
     slot = bid / T;
-    tile = bid % T;
+    unit = bid % T;
   }
 }
 
-// t-th lower tile in column-major order -> (i, j), i >= j
-__device__ __forceinline__ void lower_tile(int t, int nt, int& i, int& j) {
-  int c = 0;
-  while (t >= nt - c) {
-    t -= nt - c;
-    ++c;
+// Units of a tile-pair decomposition.  rect R x C: pairs of rows per column; lower triangle of
+// R x R: column c holds rows c..R-1.
+__host__ __device__ inline int pair_units(int R, int C, bool tri) {
+  if (!tri) return ((R + 1) / 2) * C;
+  int u = 0;
+  for (int c = 0; c < R; ++c) u += (R - c + 1) / 2;
+  return u;
+}
+__device__ __forceinline__ void pair_unit(int u, int R, int C, bool tri, int& r, int& c) {
+  if (!tri) {
+    const int P = (R + 1) / 2;
+    c = u / P;
+    r = 2 * (u - c * P);
+    return;
   }
-  j = c;
-  i = c + t;
+  int cc = 0;
+  while (u >= (R - cc + 1) / 2) {
+    u -= (R - cc + 1) / 2;
+    ++cc;
+  }
+  c = cc;
+  r = cc + 2 * u;
 }
 
 // Squared distance along one input dimension.
 //  EXPANDED: Distances.jl 0.10.5 _pairwise!(r, SqEuclidean(), a, b) on the 1-row views that
 //            GaussianProcesses' StationaryARD KernelData builds: max(a^2 + b^2 - 2(ab), 0).
+//            (s - 2t with t = fl(ab) equals fma(-2, t, s): 2t is exact.)
 //  DIRECT  : (a - b)^2.
-// The file is compiled with -ffp-contract=off so these round exactly as written.
+// The file is compiled with -ffp-contract=off so everything else rounds exactly as written.
 __device__ __forceinline__ double sqd(double a, double b, int mode) {
   if (mode == 0) {
-    const double s = a * a + b * b;
-    const double v = s - 2.0 * (a * b);
+    const double t = a * b;
+    const double v = fma(-2.0, t, a * a + b * b);
     return v > 0.0 ? v : 0.0;
   }
   const double t = a - b;
   return t * t;
 }
-
-__device__ __forceinline__ double readlane_d(double v, int lane) {
-  const long long u = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_readlane((int)(u & 0xffffffffll), lane);
-  const int hi = __builtin_amdgcn_readlane((int)(u >> 32), lane);
-  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+// same with the squares precomputed
+__device__ __forceinline__ double sqd2(double a, double a2, double b, double b2, int mode) {
+  if (mode == 0) {
+    const double v = fma(-2.0, a * b, a2 + b2);
+    return v > 0.0 ? v : 0.0;
+  }
+  const double t = a - b;
+  return t * t;
 }
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -77,106 +97,94 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
-// Deterministic sum over the 256 threads of a workgroup; every thread gets the result.
-__device__ __forceinline__ double block_sum(double v, double* red) {
-  v = wave_sum(v);
-  const int w = threadIdx.x >> 6;
-  __syncthreads();
-  if ((threadIdx.x & 63) == 0) red[w] = v;
-  __syncthreads();
-  const double r = ((red[0] + red[1]) + red[2]) + red[3];
-  __syncthreads();
-  return r;
-}
-
 // ---------------------------------------------------------------------------------------------
-// 32x32 wave tile:  acc[a][b] += A(32 x K) * B(32 x K)^T
-//   A rows a0..a0+31 with element (r, k) at A[r + k*lda] (column-major; rows contiguous),
-//   same for B.  The MFMA is issued with the operands swapped (A-op <- B rows, B-op <- A rows) so
-//   that lane&15 indexes the output ROW: acc[a][b] lane l, reg q holds
+// Wave GEMM core:  acc[a][b] += A(64 x K) * B(32 x K)^T
+//   A rows r0..r0+63 with element (r, k) at A[r + k*lda] (column-major; rows contiguous); B rows
+//   c0..c0+31 likewise.  The MFMA is issued with the operands swapped (A-op <- B rows, B-op <- A
+//   rows) so that lane&15 indexes the output ROW: acc[a][b] lane l, reg q holds
 //       C[16a + (l&15)][16b + (l>>4) + 4q]
 //   (f64 16x16x4 C/D map: row = (lane>>4) + 4 reg, col = lane & 15; verified on gfx950), which
 //   makes stores into column-major C contiguous over 16 lanes.
-//   K must be a multiple of 16; operands are prefetched one 16-deep stage ahead into registers.
+//   K is a multiple of 16; operands are prefetched one 16-deep stage ahead into registers.
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ void mma_abt(d4 (&acc)[2][2], const double* __restrict__ A, size_t lda,
-                                        const double* __restrict__ B, size_t ldb, int K) {
+constexpr int WM = 4, WN = 2;
+__device__ __forceinline__ void mma_64x32(d4 (&acc)[WM][WN], const double* __restrict__ A, size_t lda,
+                                          const double* __restrict__ B, size_t ldb, int K) {
   if (K <= 0) return;
   const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
   const double* pa = A + lr + (size_t)lk * lda;
   const double* pb = B + lr + (size_t)lk * ldb;
   const size_t sa = 4 * lda, sb = 4 * ldb;
-  double a0[4], a1[4], b0[4], b1[4];
+  double af[4][WM], bf[4][WN];
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
-    a0[s] = pa[s * sa];
-    a1[s] = pa[s * sa + 16];
-    b0[s] = pb[s * sb];
-    b1[s] = pb[s * sb + 16];
+#pragma unroll
+    for (int a = 0; a < WM; ++a) af[s][a] = pa[s * sa + 16 * a];
+#pragma unroll
+    for (int b = 0; b < WN; ++b) bf[s][b] = pb[s * sb + 16 * b];
   }
   const int nst = K >> 4;
   for (int it = 1; it < nst; ++it) {
     pa += 4 * sa;
     pb += 4 * sb;
-    double na0[4], na1[4], nb0[4], nb1[4];
+    double na[4][WM], nb[4][WN];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      na0[s] = pa[s * sa];
-      na1[s] = pa[s * sa + 16];
-      nb0[s] = pb[s * sb];
-      nb1[s] = pb[s * sb + 16];
+#pragma unroll
+      for (int a = 0; a < WM; ++a) na[s][a] = pa[s * sa + 16 * a];
+#pragma unroll
+      for (int b = 0; b < WN; ++b) nb[s][b] = pb[s * sb + 16 * b];
     }
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      acc[0][0] = mfma(b0[s], a0[s], acc[0][0]);
-      acc[0][1] = mfma(b1[s], a0[s], acc[0][1]);
-      acc[1][0] = mfma(b0[s], a1[s], acc[1][0]);
-      acc[1][1] = mfma(b1[s], a1[s], acc[1][1]);
-    }
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int a = 0; a < WM; ++a)
+#pragma unroll
+        for (int b = 0; b < WN; ++b) acc[a][b] = mfma(bf[s][b], af[s][a], acc[a][b]);
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      a0[s] = na0[s];
-      a1[s] = na1[s];
-      b0[s] = nb0[s];
-      b1[s] = nb1[s];
+#pragma unroll
+      for (int a = 0; a < WM; ++a) af[s][a] = na[s][a];
+#pragma unroll
+      for (int b = 0; b < WN; ++b) bf[s][b] = nb[s][b];
     }
   }
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    acc[0][0] = mfma(b0[s], a0[s], acc[0][0]);
-    acc[0][1] = mfma(b1[s], a0[s], acc[0][1]);
-    acc[1][0] = mfma(b0[s], a1[s], acc[1][0]);
-    acc[1][1] = mfma(b1[s], a1[s], acc[1][1]);
-  }
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int a = 0; a < WM; ++a)
+#pragma unroll
+      for (int b = 0; b < WN; ++b) acc[a][b] = mfma(bf[s][b], af[s][a], acc[a][b]);
 }
 
-__device__ __forceinline__ void acc_zero(d4 (&acc)[2][2]) {
+__device__ __forceinline__ void acc_zero(d4 (&acc)[WM][WN]) {
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < WM; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b) acc[a][b] = (d4){0.0, 0.0, 0.0, 0.0};
-}
-
-// C (column-major, ld) block of this wave  <-  scale * acc
-__device__ __forceinline__ void acc_store(const d4 (&acc)[2][2], double* C, size_t ld, double scale) {
-  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) C[(size_t)(16 * b + lk + 4 * q) * ld + 16 * a + lr] = scale * acc[a][b][q];
+    for (int b = 0; b < WN; ++b) acc[a][b] = (d4){0.0, 0.0, 0.0, 0.0};
 }
 
 // ============================================================================================
-// Gram: lower tiles of K.  grid = B * ntl, 256 threads.
+// Gram: lower tiles of K (with noise) and Kf (without).  grid = B * ntl, 256 threads, each thread
+// a 4x4 register block; X tiles in dynamic LDS as [p][64].
 // ============================================================================================
 __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
-  __shared__ double xi[DMAX * TS], xj[DMAX * TS], pw[DMAX + 4];
-  int slot, t, i, j;
-  map_block(blockIdx.x, db.B, db.ntl, slot, t);
-  lower_tile(t, db.nt, i, j);
+  extern __shared__ __attribute__((aligned(16))) double sm[];
   const int d = db.d, tid = threadIdx.x;
+  double* xi = sm;
+  double* xj = sm + d * TS;
+  double* pw = sm + 2 * d * TS;
+  int slot, t, i = 0, j = 0;
+  map_block(blockIdx.x, db.B, db.ntl, slot, t);
+  {  // t-th lower tile in column-major order
+    int c = 0, u = t;
+    while (u >= db.nt - c) {
+      u -= db.nt - c;
+      ++c;
+    }
+    j = c;
+    i = c + u;
+  }
   const double* X = db.X + (size_t)slot * db.Npad * d;
   for (int e = tid; e < TS * d; e += NTHR) {
     const int r = e / d, p = e - r * d;
@@ -187,220 +195,248 @@ __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
   for (int e = tid; e < d + 3; e += NTHR) pw[e] = P[e];
   __syncthreads();
   const double sf2 = pw[d], noise = pw[d + 1];
-  const int r = tid & 63, gi = i * TS + r, mode = db.dist_mode;
-  double* K = db.K + (size_t)slot * db.mat;
-#pragma unroll 2
-  for (int q = 0; q < 16; ++q) {
-    const int c = (tid >> 6) + 4 * q, gj = j * TS + c;
-    double v;
-    if (gi >= db.N || gj >= db.N) {
-      v = (gi == gj) ? 1.0 : 0.0;
-    } else {
-      double rr = 0.0;
-      for (int p = 0; p < d; ++p) rr = rr + sqd(xi[p * TS + r], xj[p * TS + c], mode) * pw[p];
-      v = sf2 * exp(-rr * 0.5);
-      if (gi == gj) v = v + noise;
+  const int rb = tid & 15, cb = tid >> 4, mode = db.dist_mode;
+  double rr[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) rr[a][b] = 0.0;
+  for (int p = 0; p < d; ++p) {
+    const double2 u0 = *(const double2*)(xi + p * TS + 4 * rb);
+    const double2 u1 = *(const double2*)(xi + p * TS + 4 * rb + 2);
+    const double2 v0 = *(const double2*)(xj + p * TS + 4 * cb);
+    const double2 v1 = *(const double2*)(xj + p * TS + 4 * cb + 2);
+    const double av[4] = {u0.x, u0.y, u1.x, u1.y};
+    const double bv[4] = {v0.x, v0.y, v1.x, v1.y};
+    const double w = pw[p];
+    double a2[4], b2[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      a2[a] = av[a] * av[a];
+      b2[a] = bv[a] * bv[a];
     }
-    K[(size_t)gj * db.ld + gi] = v;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) rr[a][b] = rr[a][b] + sqd2(av[a], a2[a], bv[b], b2[b], mode) * w;
+  }
+  double* K = db.K + (size_t)slot * db.mat;
+  double* KF = db.KF + (size_t)slot * db.mat;
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const int gj = j * TS + 4 * cb + b;
+    double kv[4], fv[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const int gi = i * TS + 4 * rb + a;
+      if (gi >= db.N || gj >= db.N) {
+        fv[a] = 0.0;
+        kv[a] = (gi == gj) ? 1.0 : 0.0;
+      } else {
+        fv[a] = sf2 * exp(-rr[a][b] * 0.5);
+        kv[a] = (gi == gj) ? fv[a] + noise : fv[a];
+      }
+    }
+    const size_t off = (size_t)gj * db.ld + i * TS + 4 * rb;
+    *(double2*)(K + off) = make_double2(kv[0], kv[1]);
+    *(double2*)(K + off + 2) = make_double2(kv[2], kv[3]);
+    *(double2*)(KF + off) = make_double2(fv[0], fv[1]);
+    *(double2*)(KF + off + 2) = make_double2(fv[2], fv[3]);
   }
 }
 
 // ============================================================================================
-// Left-looking Cholesky, tile column j.
-//   update: K_ij -= sum_{k<j} L_ik L_jk^T  for i >= j           grid = B * (nt - j)
-//   diag  : K_jj = L_jj L_jj^T (in registers), Dinv_j = L_jj^-1  grid = B
-//   trsm  : L_ij = K_ij Dinv_j^T  for i > j                       grid = B * (nt - j - 1)
+// Leaf of the recursion: Cholesky of the 64x64 diagonal tile jt (already reduced by the SYRK
+// updates of its ancestors) and its inverse.  One workgroup per slot; lane = column c,
+// wave w owns rows 16w..16w+15 of that column in registers.  Column k is broadcast through LDS
+// (double-buffered, one barrier per step); the update uses a_rc -= a_rk * (a_ck / a_kk) on the
+// unscaled columns, scaled once at the end.  Failure (pivot <= 0 or NaN, as LAPACK dpotrf) records
+// status 1 and the 1-based global pivot index and continues with pivot 1.
+// Writes Linv[jt,jt] = L_jj^-1 and Mt[jt,jt] = L_jj^-T (full tiles, explicit zeros) and the tile's
+// sum_c log L_cc.
 // ============================================================================================
-__global__ __launch_bounds__(NTHR) void k_potrf_update(DevBatch db, int j) {
-  int slot, t;
-  map_block(blockIdx.x, db.B, db.nt - j, slot, t);
-  const int i = j + t, w = threadIdx.x >> 6, wr = w >> 1, wc = w & 1;
-  double* K = db.K + (size_t)slot * db.mat;
-  const size_t ld = db.ld;
-  d4 acc[2][2];
-  acc_zero(acc);
-  mma_abt(acc, K + i * TS + 32 * wr, ld, K + j * TS + 32 * wc, ld, j * TS);
-  double* C = K + (size_t)(j * TS + 32 * wc) * ld + i * TS + 32 * wr;
-  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        double* pc = C + (size_t)(16 * b + lk + 4 * q) * ld + 16 * a + lr;
-        *pc = *pc - acc[a][b][q];
-      }
-}
-
-// Unblocked Cholesky of the 64x64 diagonal tile plus its triangular inverse.  Wave w owns
-// columns 16w..16w+15 of the tile, lane = row; pivot columns are broadcast through LDS (one
-// barrier per column, double-buffered).  Failure (pivot <= 0 or NaN, as LAPACK dpotrf) records
-// status 1 and the 1-based global pivot index, and continues with pivot 1.
-__global__ __launch_bounds__(NTHR) void k_potrf_diag(DevBatch db, int j) {
+constexpr int DS = TS + 1;
+__global__ __launch_bounds__(NTHR) void k_diag(DevBatch db, int jt) {
+  __shared__ double Ls[TS * DS];
   __shared__ double colbuf[2][TS];
-  __shared__ double Ls[TS * (TS + 1)];
-  __shared__ double rowbuf[4][16];
-  __shared__ double invd[TS];
+  __shared__ double piv[TS];
   __shared__ double red[4];
   const int slot = blockIdx.x, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  double* K = db.K + (size_t)slot * db.mat;
   const size_t ld = db.ld;
-  double* T = K + (size_t)j * TS * ld + j * TS;
+  const double* A = db.K + (size_t)slot * db.mat + (size_t)jt * TS * ld + jt * TS;
+  for (int e = tid; e < TS * TS; e += NTHR) {
+    const int r = e & 63, c = e >> 6;
+    Ls[c * DS + r] = (r >= c) ? A[(size_t)c * ld + r] : 0.0;
+  }
+  __syncthreads();
   double a[16];
 #pragma unroll
-  for (int q = 0; q < 16; ++q) a[q] = T[(size_t)(16 * w + q) * ld + lane];
-  double logacc = 0.0;
-  int fail_at = -1;
-#pragma unroll
+  for (int q = 0; q < 16; ++q) a[q] = Ls[lane * DS + 16 * w + q];
+  int fail = -1;
   for (int k = 0; k < TS; ++k) {
-    const int wk = k >> 4, qk = k & 15;
-    if (w == wk) {
-      double dkk = readlane_d(a[qk], k);
-      if (!(dkk > 0.0)) {
-        if (fail_at < 0) fail_at = k;
-        dkk = 1.0;
-      }
-      const double s = sqrt(dkk), inv = 1.0 / s;
-      const double lv = (lane > k) ? a[qk] * inv : (lane == k ? s : 0.0);
-      a[qk] = lv;
-      colbuf[k & 1][lane] = (lane > k) ? lv : 0.0;
-      if (lane == k) {
-        logacc += log(s);
-        invd[k] = inv;
-      }
-    }
-    __syncthreads();
-    const double lrk = colbuf[k & 1][lane];
-#pragma unroll
-    for (int q = 0; q < 16; ++q) a[q] = fma(-lrk, colbuf[k & 1][16 * w + q], a[q]);
-  }
-  // L_jj (upper triangle zero) back to K, and into LDS for the inverse
-#pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    T[(size_t)(16 * w + q) * ld + lane] = a[q];
-    Ls[(16 * w + q) * (TS + 1) + lane] = a[q];
-  }
-  // status: fail_at is wave-uniform inside the owning wave; the first failure across waves wins
-  {
-    const double lsum = wave_sum(logacc);
-    __shared__ int fails[4];
-    if (lane == 0) {
-      red[w] = lsum;
-      fails[w] = fail_at;
-    }
-    __syncthreads();
-    if (tid == 0) {
-      db.logdet_part[(size_t)slot * db.nt + j] = ((red[0] + red[1]) + red[2]) + red[3];
-      int f = -1;
-      for (int q = 0; q < 4; ++q)
-        if (fails[q] >= 0 && (f < 0 || fails[q] < f)) f = fails[q];
-      if (f >= 0 && db.status[slot] == 0) {
-        db.status[slot] = 1;
-        db.info[slot] = j * TS + f + 1;
-      }
-    }
-  }
-  // Dinv = L_jj^{-1}: wave w solves L X = I for columns 16w..16w+15, lane = row.
-  double x[16];
-#pragma unroll
-  for (int q = 0; q < 16; ++q) x[q] = (lane == 16 * w + q) ? 1.0 : 0.0;
-  const int own = w;
-#pragma unroll
-  for (int k = 0; k < TS; ++k) {
-    // row k of X for this wave's columns: lane k finalises and publishes it
+    double* cb = colbuf[k & 1];
     if (lane == k) {
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        x[q] = x[q] * invd[k];
-        rowbuf[own][q] = x[q];
+      for (int q = 0; q < 16; ++q) cb[16 * w + q] = a[q];
+    }
+    __syncthreads();
+    const double akk = cb[k];
+    const double pk = (akk > 0.0) ? akk : 1.0;
+    if (tid == 0) {
+      piv[k] = pk;
+      if (!(akk > 0.0) && fail < 0) fail = k;
+    }
+    const double t = (lane > k) ? cb[lane] / pk : 0.0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) a[q] = fma(-cb[16 * w + q], t, a[q]);
+  }
+  __syncthreads();
+  // L[r][c] = a_rc / sqrt(p_c) (r > c), sqrt(p_c) (r == c), 0 (r < c); into Ls[c][r]
+  {
+    const double sc = sqrt(piv[lane]), isc = 1.0 / sc;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int r = 16 * w + q;
+      Ls[lane * DS + r] = (r > lane) ? a[q] * isc : (r == lane ? sc : 0.0);
+    }
+    if (w == 0) {
+      const double s = wave_sum(log(sc));
+      if (lane == 0) red[0] = s;
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    db.logdet_part[(size_t)slot * db.nt + jt] = red[0];
+    if (fail >= 0 && db.status[slot] == 0) {
+      db.status[slot] = 1;
+      db.info[slot] = jt * TS + fail + 1;
+    }
+  }
+  // X = L^-1 by forward substitution: lane = column c, wave w holds rows 16w..16w+15.
+  double x[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) x[q] = (16 * w + q == lane) ? 1.0 : 0.0;
+  __shared__ double rowbuf[2][TS];
+  for (int kb = 0; kb < 4; ++kb) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int k = 16 * kb + q;
+      double* rb = rowbuf[k & 1];
+      if (w == kb) {
+        x[q] = x[q] / Ls[k * DS + k];
+        rb[lane] = x[q];
+      }
+      __syncthreads();
+      const double xr = rb[lane];
+      if (w > kb) {
+#pragma unroll
+        for (int q2 = 0; q2 < 16; ++q2) x[q2] = fma(-Ls[k * DS + 16 * w + q2], xr, x[q2]);
+      } else if (w == kb) {
+#pragma unroll
+        for (int q2 = q + 1; q2 < 16; ++q2) x[q2] = fma(-Ls[k * DS + 16 * w + q2], xr, x[q2]);
       }
     }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    const double lrk = (lane > k) ? Ls[k * (TS + 1) + lane] : 0.0;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) x[q] = fma(-lrk, rowbuf[own][q], x[q]);
-    __builtin_amdgcn_wave_barrier();
   }
-  double* Li = db.Linv + (size_t)slot * db.mat + (size_t)j * TS * ld + j * TS;
+  __syncthreads();  // all reads of Ls (L) done
 #pragma unroll
-  for (int q = 0; q < 16; ++q) Li[(size_t)(16 * w + q) * ld + lane] = x[q];
-  // Mt_jj = Dinv^T through LDS
+  for (int q = 0; q < 16; ++q) Ls[lane * DS + 16 * w + q] = x[q];  // Ls[c][r] = X[r][c]
   __syncthreads();
-#pragma unroll
-  for (int q = 0; q < 16; ++q) Ls[(16 * w + q) * (TS + 1) + lane] = x[q];  // Ls[c][r] = Dinv[r][c]
-  __syncthreads();
-  double* Mj = db.Mt + (size_t)slot * db.mat + (size_t)j * TS * ld + j * TS;
-#pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const int c = 16 * w + q;  // Mt[r][c] = Dinv[c][r] = Ls[r][c]
-    Mj[(size_t)c * ld + lane] = Ls[lane * (TS + 1) + c];
+  double* Li = db.Linv + (size_t)slot * db.mat + (size_t)jt * TS * ld + jt * TS;
+  double* Mj = db.Mt + (size_t)slot * db.mat + (size_t)jt * TS * ld + jt * TS;
+  for (int e = tid; e < TS * TS; e += NTHR) {
+    const int r = e & 63, c = e >> 6;
+    Li[(size_t)c * ld + r] = Ls[c * DS + r];  // Linv[r][c] = X[r][c]
+    Mj[(size_t)c * ld + r] = Ls[r * DS + c];  // Mt[r][c]   = X[c][r]
   }
 }
 
-__global__ __launch_bounds__(NTHR) void k_trsm(DevBatch db, int j) {
-  int slot, t;
-  map_block(blockIdx.x, db.B, db.nt - j - 1, slot, t);
-  const int i = j + 1 + t, w = threadIdx.x >> 6, wr = w >> 1, wc = w & 1;
-  double* K = db.K + (size_t)slot * db.mat;
-  const double* Li = db.Linv + (size_t)slot * db.mat;
-  const size_t ld = db.ld;
-  d4 acc[2][2];
+// ============================================================================================
+// Generic batched tile GEMM of the recursion (see GemmOp).  Unit = pair of vertically adjacent
+// 64x64 output tiles in one tile column; wave (wr, wc) = tile wr of the pair, columns 32wc..+31.
+// ============================================================================================
+__global__ __launch_bounds__(NTHR) void k_gemm(DevBatch db, GemmGeom g) {
+  const int op = g.op;
+  int r0, c0, R, C;
+  bool tri = false;
+  switch (op) {
+    case OP_TRSM:
+    case OP_LINV21: r0 = g.o + g.h; c0 = g.o; R = g.n - g.h; C = g.h; break;
+    case OP_SYRK: r0 = c0 = g.o + g.h; R = C = g.n - g.h; tri = true; break;
+    case OP_TT: r0 = g.o; c0 = g.o + g.h; R = g.h; C = g.n - g.h; break;
+    default: r0 = 0; c0 = 0; R = db.nt; C = db.mt; break;  // OP_PREDVAR
+  }
+  int slot, u, pr, pc;
+  map_block(blockIdx.x, db.B, pair_units(R, C, tri), slot, u);
+  pair_unit(u, R, C, tri, pr, pc);
+  const int w = threadIdx.x >> 6, wr = w >> 1, wc = w & 1;
+  if (pr + wr >= R) return;  // wave-uniform: second tile of an odd pair
+  const int ti = r0 + pr + wr, tj = c0 + pc;
+  const size_t ld = db.ld, so = (size_t)slot * db.mat;
+  int kb, ke;  // K range in tiles
+  const double *A, *Bm;
+  size_t ldb = ld;
+  switch (op) {
+    case OP_TRSM: kb = g.o; ke = tj + 1; A = db.K + so; Bm = db.Linv + so; break;
+    case OP_SYRK: kb = g.o; ke = g.o + g.h; A = db.Lw + so; Bm = db.Lw + so; break;
+    case OP_TT: kb = ti; ke = g.o + g.h; A = db.Mt + so; Bm = db.Lw + so; break;
+    case OP_LINV21: kb = g.o + g.h; ke = ti + 1; A = db.Linv + so; Bm = db.Lw + so; break;
+    default:
+      kb = 0;
+      ke = ti + 1;
+      A = db.Linv + so;
+      Bm = db.KsT + (size_t)slot * db.Npad * db.Mpad;
+      ldb = db.Mpad;
+      break;
+  }
+  d4 acc[WM][WN];
   acc_zero(acc);
-  mma_abt(acc, K + (size_t)j * TS * ld + i * TS + 32 * wr, ld, Li + (size_t)j * TS * ld + j * TS + 32 * wc, ld, TS);
-  __syncthreads();  // every wave has read its rows of K_ij before any wave overwrites them
-  acc_store(acc, K + (size_t)(j * TS + 32 * wc) * ld + i * TS + 32 * wr, ld, 1.0);
-}
-
-// ============================================================================================
-// Triangular inverse, sub-diagonal s:  for j, i = j + s
-//   X         = sum_{k=j}^{i-1} L_ik Linv_kj      (B-operand rows from Mt = Linv^T)
-//   Linv_ij   = -Dinv_i X,   Mt_ji = Linv_ij^T
-// grid = B * (nt - s)
-// ============================================================================================
-constexpr int XS = 80;  // LDS row stride (doubles) of the X / Y staging tile
-__global__ __launch_bounds__(NTHR) void k_trtri(DevBatch db, int s) {
-  __shared__ double Xs[TS * XS];
-  int slot, j;
-  map_block(blockIdx.x, db.B, db.nt - s, slot, j);
-  const int i = j + s, w = threadIdx.x >> 6, wr = w >> 1, wc = w & 1;
+  mma_64x32(acc, A + (size_t)kb * TS * ld + ti * TS, ld, Bm + (size_t)kb * TS * ldb + tj * TS + 32 * wc, ldb,
+            (ke - kb) * TS);
   const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
-  const double* L = db.K + (size_t)slot * db.mat;
-  double* Li = db.Linv + (size_t)slot * db.mat;
-  double* Mt = db.Mt + (size_t)slot * db.mat;
-  const size_t ld = db.ld;
-  d4 acc[2][2];
-  acc_zero(acc);
-  mma_abt(acc, L + (size_t)j * TS * ld + i * TS + 32 * wr, ld, Mt + (size_t)j * TS * ld + j * TS + 32 * wc, ld, s * TS);
-  // X -> LDS, row-major Xs[r][c]
+  if (op == OP_PREDVAR) {
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+    for (int b = 0; b < WN; ++b)
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+      for (int q = 0; q < 4; ++q) {
+        double v = 0.0;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) Xs[(32 * wr + 16 * a + lr) * XS + 32 * wc + 16 * b + lk + 4 * q] = acc[a][b][q];
-  __syncthreads();
-  // Y = Dinv_i X : A rows = Dinv_i (global, Linv_ii), B rows = X^T: Bm[c][t] = X[t][c] = Xs[t*XS + c]
-  d4 acc2[2][2];
-  acc_zero(acc2);
-  mma_abt(acc2, Li + (size_t)i * TS * ld + i * TS + 32 * wr, ld, Xs + 32 * wc, XS, TS);
-  acc_store(acc2, Li + (size_t)(j * TS + 32 * wc) * ld + i * TS + 32 * wr, ld, -1.0);
-  __syncthreads();
+        for (int a = 0; a < WM; ++a) v = fma(acc[a][b][q], acc[a][b][q], v);
+        v += __shfl_xor(v, 1);
+        v += __shfl_xor(v, 2);
+        v += __shfl_xor(v, 4);
+        v += __shfl_xor(v, 8);
+        if (lr == 0)
+          db.var_part[((size_t)slot * db.nt + ti) * db.Mpad + tj * TS + 32 * wc + 16 * b + lk + 4 * q] = v;
+      }
+    return;
+  }
+  double* Cm;
+  double sgn = 1.0;
+  switch (op) {
+    case OP_TRSM: Cm = db.Lw + so; break;
+    case OP_SYRK: Cm = db.K + so; break;
+    case OP_TT: Cm = db.Lw + so; break;
+    default: Cm = db.Linv + so; sgn = -1.0; break;
+  }
+  double* Ct = Cm + (size_t)(tj * TS + 32 * wc) * ld + ti * TS;
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < WM; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+    for (int b = 0; b < WN; ++b)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) Xs[(32 * wr + 16 * a + lr) * XS + 32 * wc + 16 * b + lk + 4 * q] = -acc2[a][b][q];
-  __syncthreads();
-  // Mt_ji[r'][c'] = Y[c'][r'] = Xs[c'*XS + r']
-  double* Mji = Mt + (size_t)i * TS * ld + j * TS;
-  const int rr = threadIdx.x & 63;
+      for (int q = 0; q < 4; ++q) {
+        double* p = Ct + (size_t)(16 * b + lk + 4 * q) * ld + 16 * a + lr;
+        if (op == OP_SYRK) *p = *p - acc[a][b][q];
+        else *p = sgn * acc[a][b][q];
+      }
+  if (op == OP_LINV21) {  // Mt[tj, ti] = Linv[ti, tj]^T
+    double* Mtt = db.Mt + so + (size_t)(ti * TS) * ld + tj * TS + 32 * wc;
 #pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const int c = (threadIdx.x >> 6) + 4 * q;
-    Mji[(size_t)c * ld + rr] = Xs[c * XS + rr];
+    for (int a = 0; a < WM; ++a)
+#pragma unroll
+      for (int b = 0; b < WN; ++b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Mtt[(size_t)(16 * a + lr) * ld + 16 * b + lk + 4 * q] = -acc[a][b][q];
   }
 }
 
@@ -427,85 +463,117 @@ __global__ __launch_bounds__(NTHR) void k_alpha(DevBatch db, int phase) {
 }
 
 // ============================================================================================
-// K^-1 lower tile (i,j) = sum_{k>=i} Mt_ik Mt_jk^T, fused with the gradient partial sums
-//   G_ij = wt_ij * (alpha_i alpha_j - Kinv_ij) * Kf_ij     (wt = 1/2 on the diagonal, as
-//                                                          dmll_kern! weights ααinvcKI[j,j]/2)
-//   S_p  = sum G_ij dist_p(x_i, x_j),  S_f = sum G_ij,  T = sum_diag W_ii
-// grid = B * ntl
+// K^-1 lower tiles = Mt_i Mt_j^T (K range [i, nt)), fused with the gradient partial sums
+//   G_rc = wt_rc * (alpha_r alpha_c - Kinv_rc) * Kf_rc    (wt = 1/2 on the diagonal, as
+//                                                        dmll_kern! weights ααinvcKI[j,j]/2)
+//   S_p = sum G_rc dist_p(x_r, x_c),  S_f = sum G_rc,  T = sum_diag W_rr
+// Unit = tile pair (ti, ti+1) x tj of the lower triangle; one gradient partial row per unit.
+// Dynamic LDS: X of the three point tiles [p][64] + their alpha.
 // ============================================================================================
-constexpr int GS = 65;
 __global__ __launch_bounds__(NTHR) void k_lauum_grad(DevBatch db) {
-  __shared__ double xi[DMAX * TS], xj[DMAX * TS];
-  __shared__ double g[TS * GS];
-  __shared__ double ai[TS], aj[TS], pw[DMAX + 4], sp[DMAX], red[4];
-  int slot, t, i, j;
-  map_block(blockIdx.x, db.B, db.ntl, slot, t);
-  lower_tile(t, db.nt, i, j);
-  const int tid = threadIdx.x, w = tid >> 6, wr = w >> 1, wc = w & 1;
-  const int l = tid & 63, lr = l & 15, lk = l >> 4;
-  const int d = db.d, mode = db.dist_mode;
-  const double* Mt = db.Mt + (size_t)slot * db.mat;
-  const size_t ld = db.ld;
-  d4 acc[2][2];
-  acc_zero(acc);
-  mma_abt(acc, Mt + (size_t)i * TS * ld + i * TS + 32 * wr, ld, Mt + (size_t)i * TS * ld + j * TS + 32 * wc, ld,
-          (db.nt - i) * TS);
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  const int d = db.d, tid = threadIdx.x, w = tid >> 6, wr = w >> 1, wc = w & 1;
+  double* xr_s = sm;                // [2][d][64] rows of ti, ti+1
+  double* xc_s = sm + 2 * d * TS;   // [d][64]    rows of tj
+  double* al_s = sm + 3 * d * TS;   // [3][64]
+  double* pw = al_s + 3 * TS;       // [d+3]
+  double* sp = pw + DMAX + 4;       // [4][d+2]
+  const int nt = db.nt;
+  int slot, u, pr, tj;
+  map_block(blockIdx.x, db.B, pair_units(nt, nt, true), slot, u);
+  pair_unit(u, nt, nt, true, pr, tj);
   const double* X = db.X + (size_t)slot * db.Npad * d;
+  const double* al = db.alpha + (size_t)slot * db.Npad;
   for (int e = tid; e < TS * d; e += NTHR) {
     const int r = e / d, p = e - r * d;
-    xi[p * TS + r] = X[(size_t)i * TS * d + e];
-    xj[p * TS + r] = X[(size_t)j * TS * d + e];
+    xr_s[p * TS + r] = X[(size_t)pr * TS * d + e];
+    xr_s[d * TS + p * TS + r] = (pr + 1 < nt) ? X[(size_t)(pr + 1) * TS * d + e] : 0.0;
+    xc_s[p * TS + r] = X[(size_t)tj * TS * d + e];
+  }
+  if (tid < TS) {
+    al_s[tid] = al[pr * TS + tid];
+    al_s[TS + tid] = (pr + 1 < nt) ? al[(pr + 1) * TS + tid] : 0.0;
+    al_s[2 * TS + tid] = al[tj * TS + tid];
   }
   const double* P = db.params + (size_t)slot * db.pst;
   for (int e = tid; e < d + 3; e += NTHR) pw[e] = P[e];
-  if (tid < TS) ai[tid] = db.alpha[(size_t)slot * db.Npad + i * TS + tid];
-  else if (tid < 2 * TS) aj[tid - TS] = db.alpha[(size_t)slot * db.Npad + j * TS + tid - TS];
+  const int ti = pr + wr;
+  const bool active = ti < nt;
+  const int l = tid & 63, lr = l & 15, lk = l >> 4, mode = db.dist_mode;
+  d4 acc[WM][WN];
+  acc_zero(acc);
+  const size_t ld = db.ld, so = (size_t)slot * db.mat;
+  if (active)
+    mma_64x32(acc, db.Mt + so + (size_t)ti * TS * ld + ti * TS, ld, db.Mt + so + (size_t)ti * TS * ld + tj * TS + 32 * wc,
+              ld, (nt - ti) * TS);
   __syncthreads();
-  const double sf2 = pw[d];
   double sf = 0.0, tr = 0.0;
+  const double* xr = xr_s + wr * d * TS;
+  const double* KF = db.KF + so + (size_t)(tj * TS + 32 * wc) * ld + ti * TS;
+  if (active) {
+    // G in place of acc
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < WM; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+      for (int b = 0; b < WN; ++b)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int r = 32 * wr + 16 * a + lr, c = 32 * wc + 16 * b + lk + 4 * q;
-        const int gi = i * TS + r, gj = j * TS + c;
-        double G = 0.0;
-        if (gi < db.N && gj < db.N && gi >= gj) {
-          double rr = 0.0;
-          for (int p = 0; p < d; ++p) rr = rr + sqd(xi[p * TS + r], xj[p * TS + c], mode) * pw[p];
-          const double kf = sf2 * exp(-rr * 0.5);
-          const double W = ai[r] * aj[c] - acc[a][b][q];
-          if (gi == gj) {
-            G = 0.5 * (W * kf);
-            tr += W;
-          } else {
-            G = W * kf;
+        for (int q = 0; q < 4; ++q) {
+          const int r = 16 * a + lr, c = 32 * wc + 16 * b + lk + 4 * q;
+          const int gi = ti * TS + r, gj = tj * TS + c;
+          double G = 0.0;
+          if (gi < db.N && gj < db.N && gi >= gj) {
+            const double kf = KF[(size_t)(16 * b + lk + 4 * q) * ld + r];
+            const double W = al_s[wr * TS + r] * al_s[2 * TS + c] - acc[a][b][q];
+            if (gi == gj) {
+              G = 0.5 * (W * kf);
+              tr += W;
+            } else {
+              G = W * kf;
+            }
+            sf += G;
           }
-          sf += G;
+          acc[a][b][q] = G;
         }
-        g[c * GS + r] = G;
-      }
-  __syncthreads();
-  // S_p: work item (p, r) -> one wave per p per pass, reduced over rows by the wave
-  for (int e = tid; e < d * TS; e += NTHR) {
-    const int p = e >> 6, r = e & 63;
-    const double x0 = xi[p * TS + r];
+  }
+  // S_p, one dimension at a time; x values of this lane's 4 rows / 8 columns from LDS
+  for (int p = 0; p < d; ++p) {
     double s = 0.0;
-    for (int c = 0; c < TS; ++c) s = fma(g[c * GS + r], sqd(x0, xj[p * TS + c], mode), s);
+    if (active) {
+      double xa[WM], xa2[WM], xb[WN][4], xb2[WN][4];
+#pragma unroll
+      for (int a = 0; a < WM; ++a) {
+        xa[a] = xr[p * TS + 16 * a + lr];
+        xa2[a] = xa[a] * xa[a];
+      }
+#pragma unroll
+      for (int b = 0; b < WN; ++b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          xb[b][q] = xc_s[p * TS + 32 * wc + 16 * b + lk + 4 * q];
+          xb2[b][q] = xb[b][q] * xb[b][q];
+        }
+#pragma unroll
+      for (int a = 0; a < WM; ++a)
+#pragma unroll
+        for (int b = 0; b < WN; ++b)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) s = fma(acc[a][b][q], sqd2(xa[a], xa2[a], xb[b][q], xb2[b][q], mode), s);
+    }
     s = wave_sum(s);
-    if (r == 0) sp[p] = s;
+    if (l == 0) sp[w * (DMAX + 2) + p] = s;
   }
-  const double sfa = block_sum(sf, red);
-  const double tra = block_sum(tr, red);
-  double* out = db.grad_part + ((size_t)slot * db.ntl + t) * db.gps;
-  for (int e = tid; e < d; e += NTHR) out[e] = sp[e];
-  if (tid == 0) {
-    out[d] = sfa;
-    out[d + 1] = tra;
+  sf = wave_sum(sf);
+  tr = wave_sum(tr);
+  if (l == 0) {
+    sp[w * (DMAX + 2) + d] = sf;
+    sp[w * (DMAX + 2) + d + 1] = tr;
   }
+  __syncthreads();
+  double* out = db.grad_part + ((size_t)slot * db.ngu + u) * db.gps;
+  for (int e = tid; e < d + 2; e += NTHR)
+    out[e] = ((sp[e] + sp[(DMAX + 2) + e]) + sp[2 * (DMAX + 2) + e]) + sp[3 * (DMAX + 2) + e];
 }
+int lauum_units(int nt) { return pair_units(nt, nt, true); }
 
 // ============================================================================================
 // Per slot: mll = -(y.alpha + logdet + N log 2pi)/2 ; gradient (d+2) in GaussianProcesses order
@@ -518,23 +586,26 @@ __global__ __launch_bounds__(NTHR) void k_finalize(DevBatch db, int want_grad) {
   const double* al = db.alpha + (size_t)slot * db.Npad;
   double s = 0.0;
   for (int k = tid; k < db.N; k += NTHR) s = fma(y[k], al[k], s);
-  const double ya = block_sum(s, red);
+  s = wave_sum(s);
+  if ((tid & 63) == 0) red[tid >> 6] = s;
+  __syncthreads();
   double* out = db.out + (size_t)slot * (d + 3);
   if (tid == 0) {
-    double ld = 0.0;
-    for (int k = 0; k < db.nt; ++k) ld += db.logdet_part[(size_t)slot * db.nt + k];
+    const double ya = ((red[0] + red[1]) + red[2]) + red[3];
+    double ldt = 0.0;
+    for (int k = 0; k < db.nt; ++k) ldt += db.logdet_part[(size_t)slot * db.nt + k];
     const double log2pi = 1.8378770664093453;  // log(2pi), Julia's log2π
-    out[0] = -((ya + 2.0 * ld) + log2pi * db.N) / 2.0;
+    out[0] = -((ya + 2.0 * ldt) + log2pi * db.N) / 2.0;
   }
   if (want_grad) {
     const double* P = db.params + (size_t)slot * db.pst;
-    const double* gp = db.grad_part + (size_t)slot * db.ntl * db.gps;
+    const double* gp = db.grad_part + (size_t)slot * db.ngu * db.gps;
     for (int q = tid; q < d + 2; q += NTHR) {
       double tot = 0.0;
-      for (int t = 0; t < db.ntl; ++t) tot += gp[(size_t)t * db.gps + q];
-      if (q < d) out[2 + q] = P[q] * tot;           // d mll / d log ell_q = il2_q * S_q
-      else if (q == d) out[2 + d] = 2.0 * tot;      // d mll / d log sf     = 2 S_f
-      else out[1] = P[d + 2] * tot;                 // d mll / d log sn     = sn2 tr(W)
+      for (int t = 0; t < db.ngu; ++t) tot += gp[(size_t)t * db.gps + q];
+      if (q < d) out[2 + q] = P[q] * tot;       // d mll / d log ell_q = il2_q * S_q
+      else if (q == d) out[2 + d] = 2.0 * tot;  // d mll / d log sf     = 2 S_f
+      else out[1] = P[d + 2] * tot;             // d mll / d log sn     = sn2 tr(W)
     }
   }
 }
@@ -543,16 +614,21 @@ __global__ __launch_bounds__(NTHR) void k_finalize(DevBatch db, int want_grad) {
 // Prediction.
 //   pred_cross: K*^T tile (64 test x 64 train) + partial means over the train tile.
 //               grid = B * nt * mt
-//   pred_var  : V = Linv K* row tile i, column sums of V^2 -> var_part.  grid = B * nt * mt
+//   (pred_var : OP_PREDVAR of k_gemm, V = Linv K*, column sums of V^2)
 //   pred_final: mu = sum mu_part, var = max(sf2 - sum var_part, 0).       grid = B
 // ============================================================================================
 __global__ __launch_bounds__(NTHR) void k_pred_cross(DevBatch db) {
-  __shared__ double xt[DMAX * TS], xs[DMAX * TS], pw[DMAX + 4], at[TS];
-  __shared__ double part[4][TS];
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  const int d = db.d, tid = threadIdx.x;
+  double* xt = sm;
+  double* xs = sm + d * TS;
+  double* pw = sm + 2 * d * TS;
+  double* at = pw + DMAX + 4;
+  double* part = at + TS;  // [16][64]
   int slot, t;
   map_block(blockIdx.x, db.B, db.nt * db.mt, slot, t);
   const int ch = t / db.mt, mtile = t - ch * db.mt;
-  const int tid = threadIdx.x, d = db.d, mode = db.dist_mode;
+  const int mode = db.dist_mode;
   const double* X = db.X + (size_t)slot * db.Npad * d;
   const double* Xq = db.Xs + (size_t)slot * db.Mpad * d;
   for (int e = tid; e < TS * d; e += NTHR) {
@@ -565,54 +641,55 @@ __global__ __launch_bounds__(NTHR) void k_pred_cross(DevBatch db) {
   if (tid < TS) at[tid] = db.alpha[(size_t)slot * db.Npad + ch * TS + tid];
   __syncthreads();
   const double sf2 = pw[d];
-  const int m = tid & 63, pt = tid >> 6, gm = mtile * TS + m;
-  double* KsT = db.KsT + (size_t)slot * db.Npad * db.Mpad;
-  double macc = 0.0;
-  for (int r = pt; r < TS; r += 4) {
-    const int gt = ch * TS + r;
-    double kv = 0.0;
-    if (gt < db.N && gm < db.M) {
-      double rr = 0.0;
-      for (int p = 0; p < d; ++p) rr = rr + sqd(xt[p * TS + r], xs[p * TS + m], mode) * pw[p];
-      kv = sf2 * exp(-rr * 0.5);
+  // thread: 4 test points (4mb..) x 4 train points (4rb..)
+  const int mb = tid & 15, rb = tid >> 4;
+  double rr[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) rr[a][b] = 0.0;
+  for (int p = 0; p < d; ++p) {
+    const double2 u0 = *(const double2*)(xt + p * TS + 4 * rb);
+    const double2 u1 = *(const double2*)(xt + p * TS + 4 * rb + 2);
+    const double2 v0 = *(const double2*)(xs + p * TS + 4 * mb);
+    const double2 v1 = *(const double2*)(xs + p * TS + 4 * mb + 2);
+    const double av[4] = {u0.x, u0.y, u1.x, u1.y};
+    const double bv[4] = {v0.x, v0.y, v1.x, v1.y};
+    const double wgt = pw[p];
+    double a2[4], b2[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      a2[a] = av[a] * av[a];
+      b2[a] = bv[a] * bv[a];
     }
-    KsT[(size_t)gt * db.Mpad + gm] = kv;
-    macc = fma(kv, at[r], macc);
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) rr[a][b] = rr[a][b] + sqd2(av[a], a2[a], bv[b], b2[b], mode) * wgt;
   }
-  part[pt][m] = macc;
-  __syncthreads();
-  if (pt == 0)
-    db.mu_part[((size_t)slot * db.nt + ch) * db.Mpad + gm] = ((part[0][m] + part[1][m]) + part[2][m]) + part[3][m];
-}
-
-__global__ __launch_bounds__(NTHR) void k_pred_var(DevBatch db) {
-  __shared__ double cs[2][2][32];
-  int slot, t;
-  map_block(blockIdx.x, db.B, db.nt * db.mt, slot, t);
-  const int i = t / db.mt, mtile = t - i * db.mt;
-  const int w = threadIdx.x >> 6, wr = w >> 1, wc = w & 1;
-  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
-  const double* Li = db.Linv + (size_t)slot * db.mat;
-  const double* KsT = db.KsT + (size_t)slot * db.Npad * db.Mpad;
-  d4 acc[2][2];
-  acc_zero(acc);
-  mma_abt(acc, Li + i * TS + 32 * wr, db.ld, KsT + mtile * TS + 32 * wc, db.Mpad, (i + 1) * TS);
-  // column sums of squares: sum over rows = over a, lr (16 lanes), wr (2 waves)
+  double* KsT = db.KsT + (size_t)slot * db.Npad * db.Mpad;
+  double macc[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-  for (int b = 0; b < 2; ++b)
+  for (int a = 0; a < 4; ++a) {  // train point gt
+    const int gt = ch * TS + 4 * rb + a;
+    double kv[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      double v = acc[0][b][q] * acc[0][b][q] + acc[1][b][q] * acc[1][b][q];
-      v += __shfl_xor(v, 1);
-      v += __shfl_xor(v, 2);
-      v += __shfl_xor(v, 4);
-      v += __shfl_xor(v, 8);
-      if (lr == 0) cs[wr][wc][16 * b + lk + 4 * q] = v;
+    for (int b = 0; b < 4; ++b) {
+      const int gm = mtile * TS + 4 * mb + b;
+      kv[b] = (gt < db.N && gm < db.M) ? sf2 * exp(-rr[a][b] * 0.5) : 0.0;
+      macc[b] = fma(kv[b], at[4 * rb + a], macc[b]);
     }
+    double* o = KsT + (size_t)gt * db.Mpad + mtile * TS + 4 * mb;
+    *(double2*)o = make_double2(kv[0], kv[1]);
+    *(double2*)(o + 2) = make_double2(kv[2], kv[3]);
+  }
+#pragma unroll
+  for (int b = 0; b < 4; ++b) part[rb * TS + 4 * mb + b] = macc[b];
   __syncthreads();
-  if (threadIdx.x < TS) {
-    const int c = threadIdx.x, cw = c >> 5, cc = c & 31;
-    db.var_part[((size_t)slot * db.nt + i) * db.Mpad + mtile * TS + c] = cs[0][cw][cc] + cs[1][cw][cc];
+  if (tid < TS) {
+    double s = 0.0;
+    for (int k = 0; k < 16; ++k) s += part[k * TS + tid];
+    db.mu_part[((size_t)slot * db.nt + ch) * db.Mpad + mtile * TS + tid] = s;
   }
 }
 
@@ -634,35 +711,51 @@ __global__ __launch_bounds__(NTHR) void k_pred_final(DevBatch db) {
 // ---------------------------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------------------------
+static size_t gram_lds(int d) { return (size_t)(2 * d * TS + DMAX + 4) * sizeof(double); }
+static size_t lauum_lds(int d) { return (size_t)(3 * d * TS + 3 * TS + DMAX + 4 + 4 * (DMAX + 2)) * sizeof(double); }
+static size_t cross_lds(int d) { return (size_t)(2 * d * TS + DMAX + 4 + TS + 16 * TS) * sizeof(double); }
+
+static void set_lds_limits() {
+  static bool done = false;
+  if (done) return;
+  done = true;
+  (void)hipFuncSetAttribute((const void*)k_gram, hipFuncAttributeMaxDynamicSharedMemorySize, (int)gram_lds(DMAX));
+  (void)hipFuncSetAttribute((const void*)k_lauum_grad, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lauum_lds(DMAX));
+  (void)hipFuncSetAttribute((const void*)k_pred_cross, hipFuncAttributeMaxDynamicSharedMemorySize, (int)cross_lds(DMAX));
+}
+
 void launch_gram(const DevBatch& b, hipStream_t s) {
-  hipLaunchKernelGGL(k_gram, dim3(b.B * b.ntl), dim3(NTHR), 0, s, b);
+  set_lds_limits();
+  hipLaunchKernelGGL(k_gram, dim3(b.B * b.ntl), dim3(NTHR), gram_lds(b.d), s, b);
 }
-void launch_potrf_update(const DevBatch& b, int j, hipStream_t s) {
-  hipLaunchKernelGGL(k_potrf_update, dim3(b.B * (b.nt - j)), dim3(NTHR), 0, s, b, j);
+void launch_diag(const DevBatch& b, int jt, hipStream_t s) {
+  hipLaunchKernelGGL(k_diag, dim3(b.B), dim3(NTHR), 0, s, b, jt);
 }
-void launch_potrf_diag(const DevBatch& b, int j, hipStream_t s) {
-  hipLaunchKernelGGL(k_potrf_diag, dim3(b.B), dim3(NTHR), 0, s, b, j);
-}
-void launch_trsm(const DevBatch& b, int j, hipStream_t s) {
-  hipLaunchKernelGGL(k_trsm, dim3(b.B * (b.nt - j - 1)), dim3(NTHR), 0, s, b, j);
-}
-void launch_trtri(const DevBatch& b, int sd, hipStream_t s) {
-  hipLaunchKernelGGL(k_trtri, dim3(b.B * (b.nt - sd)), dim3(NTHR), 0, s, b, sd);
+void launch_gemm(const DevBatch& b, const GemmGeom& g, hipStream_t s) {
+  int R, C;
+  bool tri = false;
+  switch (g.op) {
+    case OP_TRSM:
+    case OP_LINV21: R = g.n - g.h; C = g.h; break;
+    case OP_SYRK: R = C = g.n - g.h; tri = true; break;
+    case OP_TT: R = g.h; C = g.n - g.h; break;
+    default: R = b.nt; C = b.mt; break;
+  }
+  hipLaunchKernelGGL(k_gemm, dim3(b.B * pair_units(R, C, tri)), dim3(NTHR), 0, s, b, g);
 }
 void launch_alpha(const DevBatch& b, hipStream_t s, int phase) {
   hipLaunchKernelGGL(k_alpha, dim3(b.B * b.nt), dim3(NTHR), 0, s, b, phase);
 }
 void launch_lauum_grad(const DevBatch& b, hipStream_t s) {
-  hipLaunchKernelGGL(k_lauum_grad, dim3(b.B * b.ntl), dim3(NTHR), 0, s, b);
+  set_lds_limits();
+  hipLaunchKernelGGL(k_lauum_grad, dim3(b.B * lauum_units(b.nt)), dim3(NTHR), lauum_lds(b.d), s, b);
 }
 void launch_finalize(const DevBatch& b, int want_grad, hipStream_t s) {
   hipLaunchKernelGGL(k_finalize, dim3(b.B), dim3(NTHR), 0, s, b, want_grad);
 }
 void launch_pred_cross(const DevBatch& b, hipStream_t s) {
-  hipLaunchKernelGGL(k_pred_cross, dim3(b.B * b.nt * b.mt), dim3(NTHR), 0, s, b);
-}
-void launch_pred_var(const DevBatch& b, hipStream_t s) {
-  hipLaunchKernelGGL(k_pred_var, dim3(b.B * b.nt * b.mt), dim3(NTHR), 0, s, b);
+  set_lds_limits();
+  hipLaunchKernelGGL(k_pred_cross, dim3(b.B * b.nt * b.mt), dim3(NTHR), cross_lds(b.d), s, b);
 }
 void launch_pred_final(const DevBatch& b, hipStream_t s) {
   hipLaunchKernelGGL(k_pred_final, dim3(b.B), dim3(NTHR), 0, s, b);
