@@ -3,6 +3,7 @@
 #include <cfloat>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -39,6 +40,9 @@ struct gprx_ctx {
   std::map<std::string, KStat> stats;
   std::vector<hipEvent_t> evpool;
   std::vector<PendingEv> pending;
+  int nstreams = 1;                   // slot groups run concurrently on these streams (1: measured best)
+  std::vector<hipStream_t> gstreams;  // group streams
+  std::vector<hipEvent_t> gevents;    // fork/join events (1 + nstreams)
 };
 
 struct gprx_batch {
@@ -88,16 +92,53 @@ hipEvent_t ev_get(gprx_ctx* c) {
 
 // Launch helper: optional HIP-event bracket per launch, on the context stream.
 template <class F>
-void timed(gprx_ctx* c, const char* name, double flops, double bytes, F&& f) {
+void timed(gprx_ctx* c, hipStream_t st, const char* name, double flops, double bytes, F&& f) {
   if (!c->prof) {
     f();
     return;
   }
   hipEvent_t a = ev_get(c), b = ev_get(c);
-  (void)hipEventRecord(a, c->stream);
+  (void)hipEventRecord(a, st);
   f();
-  (void)hipEventRecord(b, c->stream);
+  (void)hipEventRecord(b, st);
   c->pending.push_back({name, a, b, flops, bytes});
+}
+
+// View of slots [s0, s0+cnt) of a batch (every per-slot array is slot-major).
+DevBatch sub_batch(const DevBatch& db, int s0, int cnt) {
+  DevBatch v = db;
+  const size_t s = s0;
+  v.B = cnt;
+  v.X += s * db.Npad * db.d;
+  v.Y += s * db.Npad;
+  v.K += s * db.mat;
+  v.KF += s * db.mat;
+  v.Lw += s * db.mat;
+  v.Linv += s * db.mat;
+  v.Mt += s * db.mat;
+  v.z += s * db.Npad;
+  v.alpha += s * db.Npad;
+  v.params += s * db.pst;
+  v.logdet_part += s * db.nt;
+  v.grad_part += s * db.ngu * db.gps;
+  v.Xs += s * db.Mpad * db.d;
+  v.KsT += s * db.Npad * db.Mpad;
+  v.mu_part += s * db.nt * db.Mpad;
+  v.var_part += s * db.nt * db.Mpad;
+  v.out += s * (db.d + 3);
+  v.out_mu += s * db.Mpad;
+  v.out_var += s * db.Mpad;
+  v.status += s;
+  v.info += s;
+  return v;
+}
+
+// slot groups: up to nstreams groups of >= 8 slots
+int n_groups(const gprx_ctx* c, int B) {
+  int g = B / 8;
+  if (g < 1) g = 1;
+  if (g > c->nstreams) g = c->nstreams;
+  return g;
 }
 
 void collect(gprx_ctx* c) {
@@ -179,42 +220,76 @@ int copy_in(gprx_ctx* c, void* dst, const void* src, size_t bytes, int mem) {
 }
 
 // Recursive Cholesky + inverse over tile range [o, o+n) (tile units), all slots in lock step.
-void factor_rec(gprx_ctx* c, const DevBatch& db, int o, int n) {
+void factor_rec(gprx_ctx* c, hipStream_t st, const DevBatch& db, int o, int n) {
   const double T = TS, Bd = db.B;
   if (n == 1) {
-    timed(c, "diag", Bd * (T * T * T / 3.0 + T * T * T / 3.0), Bd * 8.0 * 3.0 * T * T,
-          [&] { gprx::launch_diag(db, o, c->stream); });
+    timed(c, st, "diag", Bd * (T * T * T / 3.0 + T * T * T / 3.0), Bd * 8.0 * 3.0 * T * T,
+          [&] { gprx::launch_diag(db, o, st); });
     return;
   }
   const int h = n / 2;
   const double m1 = h * T, m2 = (n - h) * T;
-  factor_rec(c, db, o, h);
+  factor_rec(c, st, db, o, h);
   gprx::GemmGeom g{gprx::OP_TRSM, o, h, n};
-  timed(c, "potrf_trsm", Bd * m2 * m1 * m1, Bd * 8.0 * (2.0 * m2 * m1 + m1 * m1 / 2.0),
-        [&] { gprx::launch_gemm(db, g, c->stream); });
+  timed(c, st, "potrf_trsm", Bd * m2 * m1 * m1, Bd * 8.0 * (2.0 * m2 * m1 + m1 * m1 / 2.0),
+        [&] { gprx::launch_gemm(db, g, st); });
   g.op = gprx::OP_SYRK;
-  timed(c, "potrf_syrk", Bd * m2 * m2 * m1, Bd * 8.0 * (m2 * m1 + m2 * m2),
-        [&] { gprx::launch_gemm(db, g, c->stream); });
-  factor_rec(c, db, o + h, n - h);
+  timed(c, st, "potrf_syrk", Bd * m2 * m2 * m1, Bd * 8.0 * (m2 * m1 + m2 * m2),
+        [&] { gprx::launch_gemm(db, g, st); });
+  factor_rec(c, st, db, o + h, n - h);
   g.op = gprx::OP_TT;
-  timed(c, "trtri_tt", Bd * m2 * m1 * m1, Bd * 8.0 * (2.0 * m2 * m1 + m1 * m1 / 2.0),
-        [&] { gprx::launch_gemm(db, g, c->stream); });
+  timed(c, st, "trtri_tt", Bd * m2 * m1 * m1, Bd * 8.0 * (2.0 * m2 * m1 + m1 * m1 / 2.0),
+        [&] { gprx::launch_gemm(db, g, st); });
   g.op = gprx::OP_LINV21;
-  timed(c, "trtri_linv21", Bd * m1 * m2 * m2, Bd * 8.0 * (3.0 * m2 * m1 + m2 * m2 / 2.0),
-        [&] { gprx::launch_gemm(db, g, c->stream); });
+  timed(c, st, "trtri_linv21", Bd * m1 * m2 * m2, Bd * 8.0 * (3.0 * m2 * m1 + m2 * m2 / 2.0),
+        [&] { gprx::launch_gemm(db, g, st); });
 }
 
-int run_predict_kernels(gprx_batch* b) {
+void predict_group(gprx_ctx* c, hipStream_t st, const DevBatch& db) {
+  const double N = db.N, M = db.M, d = db.d, B = db.B;
+  timed(c, st, "pred_cross", B * (3.0 * N * M * d + 2.0 * N * M), B * 8.0 * (N * db.Mpad + (N + M) * d),
+        [&] { gprx::launch_pred_cross(db, st); });
+  gprx::GemmGeom g{gprx::OP_PREDVAR, 0, 0, 0};
+  timed(c, st, "pred_var", B * N * N * M, B * 8.0 * (N * N / 2 + N * db.Mpad), [&] { gprx::launch_gemm(db, g, st); });
+  timed(c, st, "pred_final", B * 2.0 * db.nt * db.Mpad, B * 16.0 * db.nt * db.Mpad,
+        [&] { gprx::launch_pred_final(db, st); });
+}
+
+// Whole evaluation of one slot group on one stream.
+void eval_group(gprx_ctx* c, hipStream_t st, const DevBatch& db, bool want_grad, bool want_pred) {
+  const double Bd = db.B, nt = db.nt, Np = db.Npad, d = db.d;
+  timed(c, st, "gram", Bd * 3.0 * db.N * (double)db.N * d / 2.0, Bd * 8.0 * (Np * Np + Np * d),
+        [&] { gprx::launch_gram(db, st); });
+  factor_rec(c, st, db, 0, db.nt);
+  timed(c, st, "alpha", Bd * Np * Np, Bd * 8.0 * Np * Np / 2.0, [&] { gprx::launch_alpha(db, st, 0); });
+  timed(c, st, "alpha", Bd * Np * Np, Bd * 8.0 * Np * Np / 2.0, [&] { gprx::launch_alpha(db, st, 1); });
+  if (want_grad)
+    timed(c, st, "lauum_grad", Bd * (Np * Np * Np / 3.0 + 2.0 * Np * Np * d + 4.0 * Np * Np),
+          Bd * 8.0 * (Np * Np / 2.0 + TS * TS * (nt * (nt + 1.0) * (nt + 2.0) / 3.0)),
+          [&] { gprx::launch_lauum_grad(db, st); });
+  timed(c, st, "finalize", Bd * 2.0 * db.N, Bd * 16.0 * db.N, [&] { gprx::launch_finalize(db, want_grad ? 1 : 0, st); });
+  if (want_pred) predict_group(c, st, db);
+}
+
+// Fork the slot groups of `b` over the context's group streams, join back on the main stream.
+int run_groups(gprx_batch* b, bool want_grad, bool want_pred, bool factor) {
   gprx_ctx* c = b->ctx;
   const DevBatch& db = b->db;
-  const double N = db.N, M = db.M, d = db.d, B = db.B;
-  timed(c, "pred_cross", B * (3.0 * N * M * d + 2.0 * N * M), B * 8.0 * (N * db.Mpad + (N + M) * d),
-        [&] { gprx::launch_pred_cross(db, c->stream); });
-  gprx::GemmGeom g{gprx::OP_PREDVAR, 0, 0, 0};
-  timed(c, "pred_var", B * N * N * M, B * 8.0 * (N * N / 2 + N * db.Mpad),
-        [&] { gprx::launch_gemm(db, g, c->stream); });
-  timed(c, "pred_final", B * 2.0 * db.nt * db.Mpad, B * 16.0 * db.nt * db.Mpad,
-        [&] { gprx::launch_pred_final(db, c->stream); });
+  const int G = n_groups(c, db.B);
+  HIPCHK(c, hipEventRecord(c->gevents[0], c->stream));
+  int s0 = 0;
+  for (int g = 0; g < G; ++g) {
+    const int cnt = db.B / G + (g < db.B % G ? 1 : 0);
+    hipStream_t st = c->gstreams[g];
+    HIPCHK(c, hipStreamWaitEvent(st, c->gevents[0], 0));
+    const DevBatch v = sub_batch(db, s0, cnt);
+    if (factor) eval_group(c, st, v, want_grad, want_pred);
+    else if (want_pred) predict_group(c, st, v);
+    HIPCHK(c, hipEventRecord(c->gevents[1 + g], st));
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->gevents[1 + g], 0));
+    s0 += cnt;
+  }
+  HIPCHK(c, hipGetLastError());
   return GPRX_OK;
 }
 
@@ -248,6 +323,13 @@ int gprx_ctx_create(int device, gprx_ctx** out) {
     delete c;
     return GPRX_DEVICE_ERROR;
   }
+  if (const char* ns = getenv("GPRX_STREAMS")) c->nstreams = atoi(ns) > 0 ? atoi(ns) : 1;
+  c->gstreams.resize(c->nstreams);
+  c->gevents.resize(1 + c->nstreams);
+  for (auto& st : c->gstreams)
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return GPRX_DEVICE_ERROR;
+  for (auto& e : c->gevents)
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return GPRX_DEVICE_ERROR;
   *out = c;
   return GPRX_OK;
 }
@@ -261,6 +343,11 @@ void gprx_ctx_destroy(gprx_ctx* c) {
     (void)hipEventDestroy(p.b);
   }
   for (auto e : c->evpool) (void)hipEventDestroy(e);
+  for (auto st : c->gstreams) {
+    (void)hipStreamSynchronize(st);
+    (void)hipStreamDestroy(st);
+  }
+  for (auto e : c->gevents) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -345,6 +432,13 @@ int gprx_batch_create(gprx_ctx* c, int B, int d, int N, int M_max, gprx_batch** 
   if ((rc = dalloc(b, &db.out, Bs * (d + 3)))) return fail(rc);
   if ((rc = dalloc(b, &db.status, 2 * Bs))) return fail(rc);
   db.info = db.status + Bs;
+  if ((rc = dalloc(b, &db.lauum_order, 2 * (size_t)db.ngu))) return fail(rc);
+  {
+    std::vector<int> ord(2 * (size_t)db.ngu);
+    gprx::lauum_order_host(db.nt, ord.data());
+    if (hipMemcpy(db.lauum_order, ord.data(), ord.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess)
+      return fail(GPRX_DEVICE_ERROR);
+  }
   if ((rc = alloc_test(b, M_max))) return fail(rc);
   if (hipHostMalloc((void**)&b->h_params, Bs * db.pst * sizeof(double)) != hipSuccess ||
       hipHostMalloc((void**)&b->h_out, Bs * (d + 3) * sizeof(double)) != hipSuccess ||
@@ -430,7 +524,7 @@ static int batch_predict_locked(gprx_batch* b, double* mu, double* var) {
   DevBatch& db = b->db;
   if (!b->factored) return set_err(c, GPRX_NOT_READY, "predict before a successful factorisation");
   if (!b->have_test || db.M == 0) return GPRX_OK;
-  int rc = run_predict_kernels(b);
+  int rc = run_groups(b, false, true, false);
   if (rc) return rc;
   HIPCHK(c, hipMemcpyAsync(b->h_mu, db.out_mu, (size_t)db.B * db.Mpad * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipMemcpyAsync(b->h_var, db.out_var, (size_t)db.B * db.Mpad * sizeof(double), hipMemcpyDeviceToHost, c->stream));
@@ -452,6 +546,10 @@ int gprx_batch_run(gprx_batch* b, const double* theta, unsigned flags, double* m
   if (hipSetDevice(c->device) != hipSuccess) return GPRX_DEVICE_ERROR;
   DevBatch& db = b->db;
   db.dist_mode = c->dist_mode;
+  {
+    const char* ab = getenv("GPRX_ABLATE");  // timing experiments only; results are wrong when set
+    db.ablate = ab ? atoi(ab) : 0;
+  }
   const int d = db.d, B = db.B, np = d + 2;
   // hyper-parameters -> kernel parameters, exactly as SEArd / GPE derive them:
   //   il2 = exp(-2 log ell), sf2 = exp(2 log sf), noise = exp(2 logNoise) + eps()
@@ -471,25 +569,15 @@ int gprx_batch_run(gprx_batch* b, const double* theta, unsigned flags, double* m
   }
   HIPCHK(c, hipMemcpyAsync(db.params, b->h_params, (size_t)B * db.pst * sizeof(double), hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemcpyAsync(db.status, b->h_status, 2 * (size_t)B * sizeof(int), hipMemcpyHostToDevice, c->stream));
-  const double Bd = B, nt = db.nt, Np = db.Npad;
-  timed(c, "gram", Bd * 3.0 * db.N * (double)db.N * d / 2.0, Bd * 8.0 * (Np * Np + Np * d),
-        [&] { gprx::launch_gram(db, c->stream); });
-  factor_rec(c, db, 0, db.nt);
-  timed(c, "alpha", Bd * Np * Np, Bd * 8.0 * Np * Np / 2.0, [&] { gprx::launch_alpha(db, c->stream, 0); });
-  timed(c, "alpha", Bd * Np * Np, Bd * 8.0 * Np * Np / 2.0, [&] { gprx::launch_alpha(db, c->stream, 1); });
   const bool want_grad = (flags & GPRX_WANT_GRAD) != 0;
-  if (want_grad)
-    timed(c, "lauum_grad", Bd * (Np * Np * Np / 3.0 + 2.0 * Np * Np * d + 4.0 * Np * Np),
-          Bd * 8.0 * (Np * Np / 2.0 + TS * TS * (nt * (nt + 1.0) * (nt + 2.0) / 3.0)),
-          [&] { gprx::launch_lauum_grad(db, c->stream); });
-  timed(c, "finalize", Bd * 2.0 * db.N, Bd * 16.0 * db.N, [&] { gprx::launch_finalize(db, want_grad ? 1 : 0, c->stream); });
-  HIPCHK(c, hipGetLastError());
+  const bool want_pred = (flags & GPRX_WANT_PREDICT) != 0 && b->have_test && db.M > 0;
+  {
+    int rc = run_groups(b, want_grad, want_pred, true);
+    if (rc) return rc;
+  }
   HIPCHK(c, hipMemcpyAsync(b->h_out, db.out, (size_t)B * (d + 3) * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipMemcpyAsync(b->h_status, db.status, 2 * (size_t)B * sizeof(int), hipMemcpyDeviceToHost, c->stream));
-  const bool want_pred = (flags & GPRX_WANT_PREDICT) != 0 && b->have_test && db.M > 0;
   if (want_pred) {
-    int rc = run_predict_kernels(b);
-    if (rc) return rc;
     HIPCHK(c, hipMemcpyAsync(b->h_mu, db.out_mu, (size_t)B * db.Mpad * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(b->h_var, db.out_var, (size_t)B * db.Mpad * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   }

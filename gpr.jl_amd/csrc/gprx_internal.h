@@ -23,6 +23,7 @@ struct DevBatch {
   int B, d, N, Npad, nt, ntl;  // nt = Npad/64 tiles per edge, ntl = nt(nt+1)/2 lower tiles
   int M, Mpad, mt;             // test points (per slot), padded to 64, mt = Mpad/64
   int dist_mode;               // GPRX_DIST_EXPANDED / GPRX_DIST_DIRECT
+  int ablate;                  // timing-only ablation bits (env GPRX_ABLATE; 0 in production)
   int pst;                     // stride of params per slot
   int gps;                     // stride of per-unit gradient partials (d + 2)
   int ngu;                     // gradient partial units per slot
@@ -49,6 +50,7 @@ struct DevBatch {
   double* out_var;             // B x Mpad
   int* status;                 // B
   int* info;                   // B
+  int* lauum_order;            // ngu x 2 (first row, column) of the lauum units, longest first
 };
 
 // GEMM operations of the recursive factorisation / inverse / prediction (tile units, see
@@ -72,6 +74,7 @@ void launch_gemm(const DevBatch& b, const GemmGeom& g, hipStream_t s);
 void launch_alpha(const DevBatch& b, hipStream_t s, int phase);
 void launch_lauum_grad(const DevBatch& b, hipStream_t s);
 int lauum_units(int nt);
+void lauum_order_host(int nt, int* out);
 void launch_finalize(const DevBatch& b, int want_grad, hipStream_t s);
 void launch_pred_cross(const DevBatch& b, hipStream_t s);
 void launch_pred_final(const DevBatch& b, hipStream_t s);

@@ -30,16 +30,15 @@ __device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
-// blockIdx -> (slot, unit); a slot's units on one XCD when B % 8 == 0 (speed only, never correctness)
-__device__ __forceinline__ void map_block(int bid, int B, int T, int& slot, int& unit) {
-  if ((B & 7) == 0) {
-    const int x = bid & 7, q = bid >> 3;
-    slot = (q / T) * 8 + x;
-    unit = q % T;
-  } else {
-    slot = bid / T;
-    unit = bid % T;
-  }
+// blockIdx -> (slot, unit).  Slot s runs on the blocks b with b % 8 == s % 8, i.e. on one XCD
+// under the dispatcher's round-robin placement (speed only, never correctness).  The grid is
+// padded to 8 * ceil(B/8) * T blocks; surplus blocks return at once.
+__host__ __device__ inline int grid_blocks(int B, int T) { return 8 * ((B + 7) / 8) * T; }
+__device__ __forceinline__ bool map_block(int bid, int B, int T, int& slot, int& unit) {
+  const int x = bid & 7, q = bid >> 3;
+  slot = (q / T) * 8 + x;
+  unit = q % T;
+  return slot < B;
 }
 
 // Units of a tile-pair decomposition.  rect R x C: pairs of rows per column; lower triangle of
@@ -175,7 +174,7 @@ __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
   double* xj = sm + d * TS;
   double* pw = sm + 2 * d * TS;
   int slot, t, i = 0, j = 0;
-  map_block(blockIdx.x, db.B, db.ntl, slot, t);
+  if (!map_block(blockIdx.x, db.B, db.ntl, slot, t)) return;
   {  // t-th lower tile in column-major order
     int c = 0, u = t;
     while (u >= db.nt - c) {
@@ -366,8 +365,19 @@ __global__ __launch_bounds__(NTHR) void k_gemm(DevBatch db, GemmGeom g) {
     default: r0 = 0; c0 = 0; R = db.nt; C = db.mt; break;  // OP_PREDVAR
   }
   int slot, u, pr, pc;
-  map_block(blockIdx.x, db.B, pair_units(R, C, tri), slot, u);
-  pair_unit(u, R, C, tri, pr, pc);
+  if (!map_block(blockIdx.x, db.B, pair_units(R, C, tri), slot, u)) return;
+  // longest K range first (the tail of a launch is its longest units)
+  if (tri) {
+    pair_unit(u, R, C, tri, pr, pc);
+  } else {
+    const int P = (R + 1) / 2, pi = u / C;
+    pc = u - pi * C;
+    switch (op) {
+      case OP_TRSM: pc = C - 1 - pc; pr = 2 * pi; break;      // K grows with the column
+      case OP_TT: pr = 2 * pi; break;                           // K shrinks with the row
+      default: pr = 2 * (P - 1 - pi); break;                    // LINV21 / PREDVAR: K grows with the row
+    }
+  }
   const int w = threadIdx.x >> 6, wr = w >> 1, wc = w & 1;
   if (pr + wr >= R) return;  // wave-uniform: second tile of an odd pair
   const int ti = r0 + pr + wr, tj = c0 + pc;
@@ -446,15 +456,22 @@ __global__ __launch_bounds__(NTHR) void k_gemm(DevBatch db, GemmGeom g) {
 __global__ __launch_bounds__(NTHR) void k_alpha(DevBatch db, int phase) {
   __shared__ double part[4][TS];
   int slot, i;
-  map_block(blockIdx.x, db.B, db.nt, slot, i);
+  if (!map_block(blockIdx.x, db.B, db.nt, slot, i)) return;
+  if (phase == 0) i = db.nt - 1 - i;  // longest rows first
   const int r = threadIdx.x & 63, pt = threadIdx.x >> 6;
   const size_t ld = db.ld;
   const double* A = (phase == 0 ? db.Linv : db.Mt) + (size_t)slot * db.mat + i * TS + r;
   const double* v = (phase == 0 ? db.Y : db.z) + (size_t)slot * db.Npad;
   const int k0 = (phase == 0) ? 0 : i * TS, k1 = (phase == 0) ? (i + 1) * TS : db.Npad;
-  double acc = 0.0;
-  for (int k = k0 + pt; k < k1; k += 4) acc = fma(A[(size_t)k * ld], v[k], acc);
-  part[pt][r] = acc;
+  // columns [k0, k1) split in 4 contiguous quarters of whole 16-column groups, 8 loads in flight
+  const int ng = (k1 - k0) / 16, g0 = (ng * pt) / 4, g1 = (ng * (pt + 1)) / 4;
+  double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int gq = g0; gq < g1; ++gq) {
+    const int kk = k0 + 16 * gq;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) acc[u & 7] = fma(A[(size_t)(kk + u) * ld], v[kk + u], acc[u & 7]);
+  }
+  part[pt][r] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
   __syncthreads();
   if (pt == 0) {
     const double s = ((part[0][r] + part[1][r]) + part[2][r]) + part[3][r];
@@ -480,8 +497,9 @@ __global__ __launch_bounds__(NTHR) void k_lauum_grad(DevBatch db) {
   double* sp = pw + DMAX + 4;       // [4][d+2]
   const int nt = db.nt;
   int slot, u, pr, tj;
-  map_block(blockIdx.x, db.B, pair_units(nt, nt, true), slot, u);
-  pair_unit(u, nt, nt, true, pr, tj);
+  if (!map_block(blockIdx.x, db.B, pair_units(nt, nt, true), slot, u)) return;
+  pr = db.lauum_order[2 * u];  // units sorted by first row (longest K range first)
+  tj = db.lauum_order[2 * u + 1];
   const double* X = db.X + (size_t)slot * db.Npad * d;
   const double* al = db.alpha + (size_t)slot * db.Npad;
   for (int e = tid; e < TS * d; e += NTHR) {
@@ -503,7 +521,7 @@ __global__ __launch_bounds__(NTHR) void k_lauum_grad(DevBatch db) {
   d4 acc[WM][WN];
   acc_zero(acc);
   const size_t ld = db.ld, so = (size_t)slot * db.mat;
-  if (active)
+  if (active && !(db.ablate & 1))
     mma_64x32(acc, db.Mt + so + (size_t)ti * TS * ld + ti * TS, ld, db.Mt + so + (size_t)ti * TS * ld + tj * TS + 32 * wc,
               ld, (nt - ti) * TS);
   __syncthreads();
@@ -538,7 +556,7 @@ __global__ __launch_bounds__(NTHR) void k_lauum_grad(DevBatch db) {
   // S_p, one dimension at a time; x values of this lane's 4 rows / 8 columns from LDS
   for (int p = 0; p < d; ++p) {
     double s = 0.0;
-    if (active) {
+    if (active && !(db.ablate & 2)) {
       double xa[WM], xa2[WM], xb[WN][4], xb2[WN][4];
 #pragma unroll
       for (int a = 0; a < WM; ++a) {
@@ -574,6 +592,17 @@ __global__ __launch_bounds__(NTHR) void k_lauum_grad(DevBatch db) {
     out[e] = ((sp[e] + sp[(DMAX + 2) + e]) + sp[2 * (DMAX + 2) + e]) + sp[3 * (DMAX + 2) + e];
 }
 int lauum_units(int nt) { return pair_units(nt, nt, true); }
+void lauum_order_host(int nt, int* out) {
+  // (first row, column) of every tile-pair unit of the lower triangle, sorted by first row
+  int k = 0;
+  for (int r = 0; r < nt; ++r)
+    for (int c = 0; c <= r; ++c)
+      if (((r - c) & 1) == 0) {
+        out[2 * k] = r;
+        out[2 * k + 1] = c;
+        ++k;
+      }
+}
 
 // ============================================================================================
 // Per slot: mll = -(y.alpha + logdet + N log 2pi)/2 ; gradient (d+2) in GaussianProcesses order
@@ -598,14 +627,24 @@ __global__ __launch_bounds__(NTHR) void k_finalize(DevBatch db, int want_grad) {
     out[0] = -((ya + 2.0 * ldt) + log2pi * db.N) / 2.0;
   }
   if (want_grad) {
+    // deterministic parallel reduction over the lauum units: 4 waves x 64 lanes stride the units,
+    // one parameter at a time
+    __shared__ double pr[4];
     const double* P = db.params + (size_t)slot * db.pst;
     const double* gp = db.grad_part + (size_t)slot * db.ngu * db.gps;
-    for (int q = tid; q < d + 2; q += NTHR) {
+    for (int q = 0; q < d + 2; ++q) {
       double tot = 0.0;
-      for (int t = 0; t < db.ngu; ++t) tot += gp[(size_t)t * db.gps + q];
-      if (q < d) out[2 + q] = P[q] * tot;       // d mll / d log ell_q = il2_q * S_q
-      else if (q == d) out[2 + d] = 2.0 * tot;  // d mll / d log sf     = 2 S_f
-      else out[1] = P[d + 2] * tot;             // d mll / d log sn     = sn2 tr(W)
+      for (int t = tid; t < db.ngu; t += NTHR) tot += gp[(size_t)t * db.gps + q];
+      tot = wave_sum(tot);
+      __syncthreads();
+      if ((tid & 63) == 0) pr[tid >> 6] = tot;
+      __syncthreads();
+      if (tid == 0) {
+        tot = ((pr[0] + pr[1]) + pr[2]) + pr[3];
+        if (q < d) out[2 + q] = P[q] * tot;       // d mll / d log ell_q = il2_q * S_q
+        else if (q == d) out[2 + d] = 2.0 * tot;  // d mll / d log sf     = 2 S_f
+        else out[1] = P[d + 2] * tot;             // d mll / d log sn     = sn2 tr(W)
+      }
     }
   }
 }
@@ -626,7 +665,7 @@ __global__ __launch_bounds__(NTHR) void k_pred_cross(DevBatch db) {
   double* at = pw + DMAX + 4;
   double* part = at + TS;  // [16][64]
   int slot, t;
-  map_block(blockIdx.x, db.B, db.nt * db.mt, slot, t);
+  if (!map_block(blockIdx.x, db.B, db.nt * db.mt, slot, t)) return;
   const int ch = t / db.mt, mtile = t - ch * db.mt;
   const int mode = db.dist_mode;
   const double* X = db.X + (size_t)slot * db.Npad * d;
@@ -726,7 +765,7 @@ static void set_lds_limits() {
 
 void launch_gram(const DevBatch& b, hipStream_t s) {
   set_lds_limits();
-  hipLaunchKernelGGL(k_gram, dim3(b.B * b.ntl), dim3(NTHR), gram_lds(b.d), s, b);
+  hipLaunchKernelGGL(k_gram, dim3(grid_blocks(b.B, b.ntl)), dim3(NTHR), gram_lds(b.d), s, b);
 }
 void launch_diag(const DevBatch& b, int jt, hipStream_t s) {
   hipLaunchKernelGGL(k_diag, dim3(b.B), dim3(NTHR), 0, s, b, jt);
@@ -741,21 +780,21 @@ void launch_gemm(const DevBatch& b, const GemmGeom& g, hipStream_t s) {
     case OP_TT: R = g.h; C = g.n - g.h; break;
     default: R = b.nt; C = b.mt; break;
   }
-  hipLaunchKernelGGL(k_gemm, dim3(b.B * pair_units(R, C, tri)), dim3(NTHR), 0, s, b, g);
+  hipLaunchKernelGGL(k_gemm, dim3(grid_blocks(b.B, pair_units(R, C, tri))), dim3(NTHR), 0, s, b, g);
 }
 void launch_alpha(const DevBatch& b, hipStream_t s, int phase) {
-  hipLaunchKernelGGL(k_alpha, dim3(b.B * b.nt), dim3(NTHR), 0, s, b, phase);
+  hipLaunchKernelGGL(k_alpha, dim3(grid_blocks(b.B, b.nt)), dim3(NTHR), 0, s, b, phase);
 }
 void launch_lauum_grad(const DevBatch& b, hipStream_t s) {
   set_lds_limits();
-  hipLaunchKernelGGL(k_lauum_grad, dim3(b.B * lauum_units(b.nt)), dim3(NTHR), lauum_lds(b.d), s, b);
+  hipLaunchKernelGGL(k_lauum_grad, dim3(grid_blocks(b.B, lauum_units(b.nt))), dim3(NTHR), lauum_lds(b.d), s, b);
 }
 void launch_finalize(const DevBatch& b, int want_grad, hipStream_t s) {
   hipLaunchKernelGGL(k_finalize, dim3(b.B), dim3(NTHR), 0, s, b, want_grad);
 }
 void launch_pred_cross(const DevBatch& b, hipStream_t s) {
   set_lds_limits();
-  hipLaunchKernelGGL(k_pred_cross, dim3(b.B * b.nt * b.mt), dim3(NTHR), cross_lds(b.d), s, b);
+  hipLaunchKernelGGL(k_pred_cross, dim3(grid_blocks(b.B, b.nt * b.mt)), dim3(NTHR), cross_lds(b.d), s, b);
 }
 void launch_pred_final(const DevBatch& b, hipStream_t s) {
   hipLaunchKernelGGL(k_pred_final, dim3(b.B), dim3(NTHR), 0, s, b);

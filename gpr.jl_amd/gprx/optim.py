@@ -1,0 +1,239 @@
+"""Host-side hyper-parameter optimiser: the call GaussianProcesses.optimize!(gp,
+LBFGS(linesearch=BackTracking(order=2)), Optim.Options(time_limit=10.)) made by every experiment
+(e.g. examples/maximal_coordinates/CPnoise.jl:41), restated from the published algorithms of
+Optim 1.4.1 (LBFGS, m = 10, InitialStatic alpha = 1, scaleinvH0) and LineSearches 7.1.1
+(BackTracking, c1 = 1e-4, rho_hi = 0.5, rho_lo = 0.1, quadratic interpolation) -- [ext, not in
+the reference tree; Manifest.toml pins the versions].
+
+Each evaluation is one device call (gprx_gp_lml / gprx_gp_lml_grad through GPE).  The objective
+follows GaussianProcesses' get_optim_target: minimise -mll; a failed evaluation (not positive
+definite, ArgumentError, non-finite hyper-parameters) counts as +Inf and the parameters are
+restored.  Besides the reference's wall-clock cap, `max_evals` gives the deterministic
+evaluation budget SURVEY.md section 8d asks for.
+"""
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib as L
+
+
+@dataclass
+class BackTracking:
+    order: int = 2
+    c_1: float = 1e-4
+    rho_hi: float = 0.5
+    rho_lo: float = 0.1
+    iterations: int = 1000
+
+    def __call__(self, phi, alpha_0: float, phi_0: float, dphi_0: float):
+        """LineSearches.BackTracking: returns (alpha, phi(alpha)); raises LineSearchError."""
+        iterfinitemax = -math.log2(np.finfo(float).eps)
+        a1 = a2 = alpha_0
+        phix0, phix1 = phi_0, phi(a1)
+        it_fin = 0
+        while not math.isfinite(phix1) and it_fin < iterfinitemax:
+            it_fin += 1
+            a1 = a2
+            a2 = a1 / 2
+            phix1 = phi(a2)
+        it = 0
+        while phix1 > phix0 + self.c_1 * a2 * dphi_0:
+            it += 1
+            if it > self.iterations:
+                raise LineSearchError(a2)
+            if self.order == 2 or it == 1:
+                atmp = -(dphi_0 * a2 * a2) / (2 * (phix1 - phix0 - dphi_0 * a2))
+            else:
+                div = 1.0 / (a1 * a1 * a2 * a2 * (a2 - a1))
+                a = (a1 * a1 * (phix1 - phi_0 - dphi_0 * a2) - a2 * a2 * (phix0 - phi_0 - dphi_0 * a1)) * div
+                b = (-a1**3 * (phix1 - phi_0 - dphi_0 * a2) + a2**3 * (phix0 - phi_0 - dphi_0 * a1)) * div
+                if abs(a) <= np.finfo(float).eps:
+                    atmp = dphi_0 / (2 * b)
+                else:
+                    disc = max(b * b - 3 * a * dphi_0, 0.0)
+                    atmp = (-b + math.sqrt(disc)) / (3 * a)
+            atmp = _nanmin(atmp, a2 * self.rho_hi)
+            a1 = a2
+            a2 = _nanmax(atmp, a2 * self.rho_lo)
+            phix0, phix1 = phix1, phi(a2)
+        return a2, phix1
+
+
+class LineSearchError(Exception):
+    def __init__(self, alpha):
+        super().__init__("line search failed to converge")
+        self.alpha = alpha
+
+
+def _nanmin(a, b):
+    return b if math.isnan(a) else (a if math.isnan(b) else min(a, b))
+
+
+def _nanmax(a, b):
+    return b if math.isnan(a) else (a if math.isnan(b) else max(a, b))
+
+
+@dataclass
+class LBFGS:
+    m: int = 10
+    linesearch: BackTracking = field(default_factory=lambda: BackTracking(order=2))
+    alphaguess: float = 1.0
+    scaleinvH0: bool = True
+
+
+@dataclass
+class Options:
+    iterations: int = 1000
+    g_abstol: float = 1e-8
+    time_limit: float = math.nan
+    max_evals: int | None = None  # deterministic budget (not in Optim)
+
+
+@dataclass
+class Result:
+    minimizer: np.ndarray
+    minimum: float
+    iterations: int
+    f_calls: int
+    g_calls: int
+    converged: bool
+    stopped_by: str
+
+
+class _Budget(Exception):
+    pass
+
+
+def _twoloop(g, rho, dxh, dgh, m, pseudo_it, scaleinvH0):
+    """Optim's twoloop!: s = -H g from the last m (dx, dg) pairs."""
+    q = g.copy()
+    lower, upper = pseudo_it - m, pseudo_it - 1
+    alpha = np.zeros(m)
+    for index in range(upper, lower - 1, -1):
+        if index < 1:
+            continue
+        i = (index - 1) % m
+        alpha[i] = rho[i] * float(dxh[i] @ q)
+        q -= alpha[i] * dgh[i]
+    if scaleinvH0 and pseudo_it > 1:
+        i = (upper - 1) % m
+        s = (float(dxh[i] @ dgh[i]) / float(dgh[i] @ dgh[i])) * q
+    else:
+        s = q.copy()
+    for index in range(lower, upper + 1):
+        if index < 1:
+            continue
+        i = (index - 1) % m
+        beta = rho[i] * float(dgh[i] @ s)
+        s += dxh[i] * (alpha[i] - beta)
+    return -s
+
+
+def lbfgs_minimize(f, fg, x0, method: LBFGS | None = None, options: Options | None = None) -> Result:
+    """Optim.optimize(OnceDifferentiable(f, g!, fg!), x0, LBFGS(...), options).
+
+    f(x) -> value; fg(x) -> (value, gradient).  Values may be +inf (failed evaluations)."""
+    method = method or LBFGS()
+    options = options or Options()
+    t0 = time.time()
+    calls = {"f": 0, "g": 0}
+
+    def count(kind):
+        calls[kind] += 1
+        if options.max_evals is not None and calls["f"] + calls["g"] > options.max_evals:
+            raise _Budget()
+
+    def F(x):
+        count("f")
+        return f(x)
+
+    def FG(x):
+        count("g")
+        return fg(x)
+
+    x = np.array(x0, dtype=np.float64)
+    n = x.shape[0]
+    m = method.m
+    dxh = [np.zeros(n) for _ in range(m)]
+    dgh = [np.zeros(n) for _ in range(m)]
+    rho = np.zeros(m)
+    stopped = "iterations"
+    it = 0
+    try:
+        fx, g = FG(x)
+        pseudo = 0
+        converged = bool(np.max(np.abs(g)) <= options.g_abstol)
+        while not converged and it < options.iterations:
+            it += 1
+            pseudo += 1
+            s = _twoloop(g, rho, dxh, dgh, m, pseudo, method.scaleinvH0)
+            g_prev = g.copy()
+            dphi0 = float(g @ s)
+            if dphi0 >= 0:  # reset_search_direction!
+                pseudo = 1
+                s = -g
+                dphi0 = float(g @ s)
+            phi = lambda a: F(x + a * s)
+            try:
+                alpha, _ = method.linesearch(phi, method.alphaguess, fx, dphi0)
+                ls_ok = True
+            except LineSearchError as e:
+                alpha, ls_ok = e.alpha, False
+            dx = alpha * s
+            x = x + dx
+            fx, g = FG(x)
+            dg = g - g_prev
+            denom = float(dx @ dg)
+            r = 1.0 / denom if denom != 0 else math.inf
+            if not math.isinf(r):
+                i = (pseudo - 1) % m
+                dxh[i] = dx.copy()
+                dgh[i] = dg.copy()
+                rho[i] = r
+            if np.max(np.abs(g)) <= options.g_abstol:
+                converged, stopped = True, "g_tol"
+            elif not ls_ok:
+                stopped = "linesearch"
+                break
+            if not math.isnan(options.time_limit) and time.time() - t0 > options.time_limit:
+                stopped = "time_limit"
+                break
+    except _Budget:
+        stopped = "max_evals"
+        converged = False
+    return Result(x, float(fx), it, calls["f"], calls["g"], converged, stopped)
+
+
+def optimize(gp, method: LBFGS | None = None, options: Options | None = None) -> Result:
+    """GaussianProcesses.optimize!(gp, method, options): minimise -mll over
+    [logσn, logℓ..., logσf]; evaluations that fail count as +Inf (get_optim_target)."""
+    init = gp.get_params().copy()
+
+    def safe(hyp, want_grad):
+        prev = gp.get_params().copy()
+        try:
+            if not np.all(np.isfinite(hyp)):
+                raise ValueError("non-finite hyperparameters")
+            gp.set_params(hyp)
+            if want_grad:
+                m, dm = gp.update_mll_and_dmll()
+                return -m, -np.asarray(dm)
+            return -gp.update_mll(), None
+        except (L.NotPositiveDefinite, ValueError):
+            gp.set_params(prev)
+            return math.inf, np.full(hyp.shape[0], math.nan)
+
+    res = lbfgs_minimize(lambda h: safe(h, False)[0], lambda h: safe(h, True), init, method, options)
+    try:
+        gp.set_params(res.minimizer)
+        gp.update_mll()
+    except Exception:
+        gp.set_params(init)
+        gp.update_mll()
+        raise
+    return res

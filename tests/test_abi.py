@@ -1,0 +1,69 @@
+"""The C-ABI library loads and exports every entry point include/gprx.h declares; host-only
+helpers (CState packing, output selection) are bit-exact copies.  No GPU compute here."""
+import ctypes as C
+import pathlib
+import re
+
+import numpy as np
+import pytest
+
+from gprx import _lib as L
+from oracle import gp_oracle as O
+
+HEADER = pathlib.Path(__file__).resolve().parents[1] / "include" / "gprx.h"
+
+
+def declared_functions():
+    txt = re.sub(r"/\*.*?\*/", "", HEADER.read_text(), flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\**\s*(gprx_[a-z_0-9]+)\s*\(", txt, flags=re.M)))
+
+
+def test_header_lists_the_abi():
+    names = declared_functions()
+    assert "gprx_batch_run" in names and "gprx_gp_lml_grad" in names and len(names) >= 20
+
+
+def test_library_exports_every_declared_symbol():
+    lib = C.CDLL(str(L.LIB_PATH))
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+    assert set(declared_functions()) == set(L.SIGNATURES), "ctypes table out of sync with gprx.h"
+
+
+def test_abi_version_and_status_strings():
+    assert L.lib.gprx_abi_version() == 1
+    assert L.lib.gprx_status_string(1) == b"not positive definite"
+
+
+def test_cstate_pack_bit_exact():
+    rng = np.random.default_rng(0)
+    nb = 4
+    xc, q, vc, wc = (rng.standard_normal((nb, k)) for k in (3, 4, 3, 3))
+    out = np.empty(13 * nb)
+    rc = L.lib.gprx_cstate_pack(nb, L.dptr(np.ascontiguousarray(xc)), L.dptr(np.ascontiguousarray(q)),
+                                L.dptr(np.ascontiguousarray(vc)), L.dptr(np.ascontiguousarray(wc)), L.dptr(out))
+    assert rc == 0
+    np.testing.assert_array_equal(out, O.cstate_pack(xc, q, vc, wc))
+
+
+def test_select_outputs_bit_exact_and_validates():
+    rng = np.random.default_rng(1)
+    d, N = 52, 33
+    Xc = rng.standard_normal((d, N))
+    idx = np.array([9, 10, 22, 23, 35, 36, 48, 49, 11, 24, 37, 50], dtype=np.int32)  # FBnoise.jl:24
+    Y = np.empty((idx.shape[0], N))
+    Xabi = np.ascontiguousarray(Xc.T)  # ABI: d x N column-major
+    assert L.lib.gprx_select_outputs(L.dptr(Xabi), d, N, L.iptr(idx), idx.shape[0], L.dptr(Y)) == 0
+    np.testing.assert_array_equal(Y, O.select_outputs(Xc, idx))
+    bad = np.array([0], dtype=np.int32)  # 1-based: 0 is invalid
+    assert L.lib.gprx_select_outputs(L.dptr(Xabi), d, N, L.iptr(bad), 1, L.dptr(Y)) == L.INVALID_ARGUMENT
+
+
+def test_ctx_create_fails_cleanly_without_gpu():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    h = C.c_void_p()
+    rc = L.lib.gprx_ctx_create(0, C.byref(h))
+    assert rc in (L.DEVICE_ERROR, L.INVALID_ARGUMENT) and not h.value

@@ -1,0 +1,194 @@
+"""Parity of the gfx950 path (through the C ABI) with the oracle restatement.
+
+Tolerances (fp64; DESIGN.md 'Parity'):
+  mll   |Δ| <= 1e-9  * max(1, |mll|)
+  grad  |Δ| <= 1e-7  * max(1, max|grad|)
+  mu    |Δ| <= 1e-9  * max|y|
+  var   |Δ| <= 1e-9  * σf²
+Status / pivot index / CState indexing: exact.
+"""
+import math
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+from oracle import gp_oracle as O  # noqa: E402
+
+TOL_MLL, TOL_GRAD, TOL_MU, TOL_VAR = 1e-9, 1e-7, 1e-9, 1e-9
+
+
+@pytest.fixture(scope="module")
+def gprx():
+    import gprx as g
+
+    return g
+
+
+@pytest.fixture(scope="module")
+def ctx(gprx):
+    c = gprx.Context(0)
+    yield c
+    c.close()
+
+
+def check_slot(r, s, X, y, theta, Xs, mode):
+    f = O.fit(X, y, theta, Xs, mode)
+    assert r["status"][s] == 0
+    assert abs(r["mll"][s] - f["mll"]) <= TOL_MLL * max(1.0, abs(f["mll"]))
+    if r["grad"] is not None:
+        gs = max(1.0, np.max(np.abs(f["grad"])))
+        assert np.max(np.abs(r["grad"][s] - f["grad"])) <= TOL_GRAD * gs
+    if r["mu"] is not None:
+        assert np.max(np.abs(r["mu"][s] - f["mu"])) <= TOL_MU * np.max(np.abs(y))
+        sf2 = math.exp(2 * theta[-1])
+        assert np.max(np.abs(r["var"][s] - f["var"])) <= TOL_VAR * sf2
+
+
+@pytest.mark.parametrize("name", ["p1_n50", "cp_n64", "p2_n100", "p2_n256", "fb_n64"])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_golden_batch(gprx, ctx, golden_dir, name, mode):
+    z = np.load(golden_dir / f"{name}.npz")
+    ctx.set_dist_mode(mode)
+    tag = "exp" if mode == 0 else "dir"
+    X, Y, Xs, th = z["X"], z["Y"], z["Xs"], z["theta"]
+    G, N = Y.shape
+    b = gprx.GPBatch(G, X.shape[0], N, Xs.shape[1], ctx=ctx)
+    b.set_train(X, Y)  # shared X: the G outputs of one trial
+    b.set_test(Xs)
+    r = b.run(np.tile(th, (G, 1)), grad=True, predict=True)
+    assert np.all(r["status"] == 0)
+    for g in range(G):
+        assert abs(r["mll"][g] - z[f"mll_{tag}"][g]) <= TOL_MLL * max(1.0, abs(z[f"mll_{tag}"][g]))
+        gs = max(1.0, np.max(np.abs(z[f"grad_{tag}"][g])))
+        assert np.max(np.abs(r["grad"][g] - z[f"grad_{tag}"][g])) <= TOL_GRAD * gs
+        assert np.max(np.abs(r["mu"][g] - z[f"mu_{tag}"][g])) <= TOL_MU * np.max(np.abs(Y[g]))
+        assert np.max(np.abs(r["var"][g] - z[f"var_{tag}"][g])) <= TOL_VAR * math.exp(2 * th[-1])
+    ctx.set_dist_mode(0)
+
+
+@pytest.mark.parametrize("N", [1, 2, 5, 33, 63, 64, 65, 127, 130, 200, 320])
+def test_ragged_sizes_per_slot_inputs(gprx, ctx, N):
+    from gprx import data
+
+    B, M = 3, 7
+    trs = [data.make_trial("CP", N, M, seed=200 + s) for s in range(B)]
+    X = np.stack([t["X"] for t in trs])
+    Y = np.stack([t["Y"][s % 4] for s, t in enumerate(trs)])
+    Xs = np.stack([t["Xs"] for t in trs])
+    rng = np.random.default_rng(N)
+    th = np.stack([data.theta0("CP", 512) + 0.1 * rng.standard_normal(28) for _ in range(B)])
+    b = gprx.GPBatch(B, 26, N, M, ctx=ctx)
+    b.set_train(X, Y)
+    b.set_test(Xs)
+    r = b.run(th, grad=True, predict=True)
+    for s in range(B):
+        check_slot(r, s, X[s], Y[s], th[s], Xs[s], 0)
+
+
+def test_full_size_p2_against_oracle_and_determinism(gprx, ctx):
+    """BASELINE size N=2048, d=26, M=100: one slot against the oracle, and 8 slots bit-identical
+    to each other and across repeated runs (size-independent properties)."""
+    from gprx import data
+
+    tr = data.make_trial("P2", 2048, 100, seed=data.trial_seed("P2", 0))
+    th = data.theta0("P2", 2048)
+    B = 8
+    b = gprx.GPBatch(B, 26, 2048, 100, ctx=ctx)
+    b.set_train(tr["X"], np.tile(tr["Y"][0], (B, 1)))
+    b.set_test(tr["Xs"])
+    r1 = b.run(np.tile(th, (B, 1)), grad=True, predict=True)
+    r2 = b.run(np.tile(th, (B, 1)), grad=True, predict=True)
+    check_slot(r1, 0, tr["X"], tr["Y"][0], th, tr["Xs"], 0)
+    for k in ("mll", "grad", "mu", "var"):
+        np.testing.assert_array_equal(r1[k], r2[k])
+        for s in range(1, B):
+            np.testing.assert_array_equal(r1[k][s], r1[k][0])
+    # predictive variance at training inputs is small; mean reproduces the noisy targets closely
+    b.set_test(tr["X"][:, :64])
+    mu, var = b.predict()
+    assert np.all(var[0] >= 0) and np.all(var[0] < math.exp(2 * th[-1]))
+
+
+def test_not_positive_definite_status_and_pivot(gprx, ctx, golden_dir):
+    z = np.load(golden_dir / "nonpd_p1.npz")
+    X, Y, th = z["X"], z["Y"], z["theta"]
+    B = 2
+    b = gprx.GPBatch(B, X.shape[0], X.shape[1], 0, ctx=ctx)
+    b.set_train(X, Y[:B])
+    good = th.copy()
+    good[0] = -2.0
+    r = b.run(np.stack([th, good]), grad=True)
+    assert r["status"][0] == 1 and 21 <= r["info"][0] <= X.shape[1]
+    assert r["status"][1] == 0
+    check_slot(r, 1, X, Y[1], good, None, 0)
+
+
+def test_nonfinite_theta_is_invalid_argument(gprx, ctx, golden_dir):
+    z = np.load(golden_dir / "p1_n50.npz")
+    b = gprx.GPBatch(2, 13, 50, 0, ctx=ctx)
+    b.set_train(z["X"], z["Y"][:2])
+    th = np.tile(z["theta"], (2, 1))
+    th[1, 3] = np.nan
+    r = b.run(th, grad=True)
+    assert r["status"][0] == 0 and r["status"][1] == 2
+
+
+def test_gpe_mirror_api(gprx, ctx, golden_dir):
+    z = np.load(golden_dir / "p2_n100.npz")
+    X, y, th, Xs = z["X"], z["Y"][2], z["theta"], z["Xs"]
+    mean = gprx.MeanFunction(lambda x: 0.1 * x[8])  # θ-independent prior mean (MeanDynamics role)
+    gp = gprx.GP(X, y, mean, gprx.SEArd(th[1:-1], th[-1]), ctx=ctx)
+    mu0 = np.array([0.1 * X[8, t] for t in range(X.shape[1])])
+    f = O.fit(X, y - mu0, th, Xs, 0)
+    assert abs(gp.mll - f["mll"]) <= TOL_MLL * abs(f["mll"])
+    gp.update_mll_and_dmll()
+    assert np.max(np.abs(gp.dmll - f["grad"])) <= TOL_GRAD * np.max(np.abs(f["grad"]))
+    mu_y, var_y = gprx.predict_y(gp, Xs)
+    ms = np.array([0.1 * Xs[8, m] for m in range(Xs.shape[1])])
+    np.testing.assert_allclose(mu_y, f["mu"] + ms, rtol=0, atol=TOL_MU * np.max(np.abs(y)))
+    np.testing.assert_allclose(var_y, f["var"] + math.exp(2 * th[0]), rtol=0, atol=TOL_VAR * math.exp(2 * th[-1]))
+    # single-column prediction, the predictdynamics.jl:13 call shape
+    m1, v1 = gp.predict_y(Xs[:, 3])
+    assert m1.shape == (1,) and abs(m1[0] - mu_y[3]) <= 1e-12 * max(1, abs(mu_y[3]))
+
+
+def test_optimize_with_budget_improves_mll(gprx, ctx, golden_dir):
+    from gprx.optim import LBFGS, Options, optimize
+
+    z = np.load(golden_dir / "cp_n64.npz")
+    th = z["theta"]
+    gp = gprx.GP(z["X"], z["Y"][0], gprx.MeanZero(), gprx.SEArd(th[1:-1], th[-1]), ctx=ctx)
+    m0 = gp.mll
+    res = optimize(gp, LBFGS(), Options(max_evals=30))
+    assert gp.mll >= m0 and res.f_calls + res.g_calls <= 31
+    np.testing.assert_allclose(gp.get_params(), res.minimizer)
+
+
+def test_device_pointer_inputs(gprx, ctx, golden_dir):
+    import torch
+
+    z = np.load(golden_dir / "p2_n256.npz")
+    X, Y, th, Xs = z["X"], z["Y"], z["theta"], z["Xs"]
+    G, N = Y.shape
+    Xd = torch.from_numpy(np.ascontiguousarray(X.T)).cuda()  # ABI layout: N x d row-major
+    Yd = torch.from_numpy(Y).cuda()
+    Xsd = torch.from_numpy(np.ascontiguousarray(Xs.T)).cuda()
+    torch.cuda.synchronize()
+    b = gprx.GPBatch(G, X.shape[0], N, Xs.shape[1], ctx=ctx)
+    b.set_train_device(Xd.data_ptr(), 0, Yd.data_ptr(), N)
+    b.set_test_device(Xsd.data_ptr(), Xs.shape[1], 0)
+    r = b.run(np.tile(th, (G, 1)), grad=True, predict=True)
+    np.testing.assert_allclose(r["mll"], z["mll_exp"], rtol=TOL_MLL)
+    np.testing.assert_allclose(r["mu"], z["mu_exp"], rtol=0, atol=TOL_MU * np.max(np.abs(Y)))
+
+
+def test_gpu_evaluator_for_sharding(gprx, ctx, golden_dir):
+    from gprx import shard
+
+    z = np.load(golden_dir / "fb_n64.npz")
+    ev = shard.gpu_evaluator(ctx=ctx)
+    G = z["Y"].shape[0]
+    r = ev(z["X"], z["Y"], np.tile(z["theta"], (G, 1)), z["Xs"])
+    np.testing.assert_allclose(r["mll"], z["mll_exp"], rtol=TOL_MLL)

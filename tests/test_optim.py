@@ -1,0 +1,72 @@
+"""Host optimiser (Optim LBFGS + LineSearches BackTracking(order=2) restatement) -- CPU only,
+driven by analytic functions and by the oracle GP target."""
+import math
+
+import numpy as np
+import pytest
+
+from gprx.optim import BackTracking, LBFGS, Options, lbfgs_minimize
+from oracle import gp_oracle as O
+
+
+def rosen(x):
+    return float(100 * (x[1] - x[0] ** 2) ** 2 + (1 - x[0]) ** 2)
+
+
+def rosen_fg(x):
+    g = np.array([-400 * x[0] * (x[1] - x[0] ** 2) - 2 * (1 - x[0]), 200 * (x[1] - x[0] ** 2)])
+    return rosen(x), g
+
+
+def test_lbfgs_rosenbrock():
+    r = lbfgs_minimize(rosen, rosen_fg, np.array([-1.2, 1.0]))
+    assert r.converged and r.stopped_by == "g_tol"
+    np.testing.assert_allclose(r.minimizer, [1.0, 1.0], atol=1e-6)
+
+
+def test_lbfgs_quadratic_exact():
+    A = np.diag([1.0, 10.0, 100.0])
+    f = lambda x: 0.5 * float(x @ A @ x)
+    r = lbfgs_minimize(f, lambda x: (f(x), A @ x), np.ones(3), options=Options(g_abstol=1e-10))
+    assert r.converged and np.max(np.abs(r.minimizer)) < 1e-9
+
+
+def test_backtracking_quadratic_interpolation_step():
+    # phi(a) = (a - 0.3)^2 from phi(0) = 0.09, phi'(0) = -0.6: one quadratic step hits 0.3 exactly
+    phi = lambda a: (a - 0.3) ** 2
+    a, v = BackTracking()(phi, 1.0, 0.09, -0.6)
+    assert a == pytest.approx(0.3) and v == pytest.approx(0.0, abs=1e-15)
+
+
+def test_backtracking_recovers_from_infinite_values():
+    phi = lambda a: math.inf if a > 0.2 else (a - 0.1) ** 2
+    a, v = BackTracking()(phi, 1.0, 0.01, -0.2)
+    assert a <= 0.2 and math.isfinite(v) and v < 0.01
+
+
+def test_max_evals_budget_is_deterministic():
+    r1 = lbfgs_minimize(rosen, rosen_fg, np.array([-1.2, 1.0]), options=Options(max_evals=15))
+    r2 = lbfgs_minimize(rosen, rosen_fg, np.array([-1.2, 1.0]), options=Options(max_evals=15))
+    assert r1.stopped_by == "max_evals" and r1.f_calls + r1.g_calls <= 16
+    np.testing.assert_array_equal(r1.minimizer, r2.minimizer)
+
+
+def test_lbfgs_improves_gp_target(golden_dir):
+    z = np.load(golden_dir / "p1_n50.npz")
+    X, y, th0 = z["X"], z["Y"][0], z["theta"]
+
+    def f(h):
+        try:
+            return -O.lml(X, y, h)[0]
+        except O.NotPosDef:
+            return math.inf
+
+    def fg(h):
+        try:
+            m, g, _ = O.lml(X, y, h, want_grad=True)
+            return -m, -g
+        except O.NotPosDef:
+            return math.inf, np.full(h.shape[0], np.nan)
+
+    r = lbfgs_minimize(f, fg, th0, LBFGS(), Options(max_evals=40))
+    assert r.minimum < f(th0)
