@@ -62,6 +62,14 @@ SIGNATURES = {
 
 
 def _load():
+    # PyTorch-ROCm ships its own libamdhip64 / libhsa-runtime64 (SONAME libamdhip64.so.7).  Loading
+    # torch first makes libgprx.so bind to that same runtime (one HSA runtime per process), so
+    # device pointers can be shared with torch and torch.distributed sees the GPUs.  Without torch
+    # (e.g. a Julia ccall host) the library uses /opt/rocm's runtime.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not LIB_PATH.exists():
         raise ImportError(
             f"gprx: native library {LIB_PATH} not found -- build it with "
