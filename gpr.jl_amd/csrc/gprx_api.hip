@@ -24,6 +24,7 @@ struct KStat {
 };
 struct PendingEv {
   std::string name;
+  std::string level;  // optional second key, e.g. "potrf_syrk/n32" (per recursion level)
   hipEvent_t a, b;
   double flops, bytes;
 };
@@ -41,6 +42,7 @@ struct gprx_ctx {
   std::vector<hipEvent_t> evpool;
   std::vector<PendingEv> pending;
   int nstreams = 1;                   // slot groups run concurrently on these streams (1: measured best)
+  int leaf_tiles = 4;                 // recursion nodes of <= this many tiles run fused (k_leaf)
   std::vector<hipStream_t> gstreams;  // group streams
   std::vector<hipEvent_t> gevents;    // fork/join events (1 + nstreams)
 };
@@ -92,7 +94,7 @@ hipEvent_t ev_get(gprx_ctx* c) {
 
 // Launch helper: optional HIP-event bracket per launch, on the context stream.
 template <class F>
-void timed(gprx_ctx* c, hipStream_t st, const char* name, double flops, double bytes, F&& f) {
+void timed(gprx_ctx* c, hipStream_t st, const char* name, double flops, double bytes, F&& f, int level = 0) {
   if (!c->prof) {
     f();
     return;
@@ -101,7 +103,7 @@ void timed(gprx_ctx* c, hipStream_t st, const char* name, double flops, double b
   (void)hipEventRecord(a, st);
   f();
   (void)hipEventRecord(b, st);
-  c->pending.push_back({name, a, b, flops, bytes});
+  c->pending.push_back({name, level ? std::string(name) + "/n" + std::to_string(level) : std::string(), a, b, flops, bytes});
 }
 
 // View of slots [s0, s0+cnt) of a batch (every per-slot array is slot-major).
@@ -145,11 +147,14 @@ void collect(gprx_ctx* c) {
   for (auto& p : c->pending) {
     float ms = 0.f;
     (void)hipEventElapsedTime(&ms, p.a, p.b);
-    KStat& s = c->stats[p.name];
-    s.ms += ms;
-    s.n += 1;
-    s.flops += p.flops;
-    s.bytes += p.bytes;
+    for (int k = 0; k < 2; ++k) {
+      if (k == 1 && p.level.empty()) break;
+      KStat& s = c->stats[k ? p.level : p.name];
+      s.ms += ms;
+      s.n += 1;
+      s.flops += p.flops;
+      s.bytes += p.bytes;
+    }
     c->evpool.push_back(p.a);
     c->evpool.push_back(p.b);
   }
@@ -222,6 +227,12 @@ int copy_in(gprx_ctx* c, void* dst, const void* src, size_t bytes, int mem) {
 // Recursive Cholesky + inverse over tile range [o, o+n) (tile units), all slots in lock step.
 void factor_rec(gprx_ctx* c, hipStream_t st, const DevBatch& db, int o, int n) {
   const double T = TS, Bd = db.B;
+  if (n > 1 && n <= c->leaf_tiles) {
+    const double m = n * T;
+    timed(c, st, "leaf", Bd * (m * m * m / 3.0 + m * m * m / 3.0), Bd * 8.0 * 3.0 * m * m,
+          [&] { gprx::launch_leaf(db, o, n, st); }, n);
+    return;
+  }
   if (n == 1) {
     timed(c, st, "diag", Bd * (T * T * T / 3.0 + T * T * T / 3.0), Bd * 8.0 * 3.0 * T * T,
           [&] { gprx::launch_diag(db, o, st); });
@@ -232,17 +243,17 @@ void factor_rec(gprx_ctx* c, hipStream_t st, const DevBatch& db, int o, int n) {
   factor_rec(c, st, db, o, h);
   gprx::GemmGeom g{gprx::OP_TRSM, o, h, n};
   timed(c, st, "potrf_trsm", Bd * m2 * m1 * m1, Bd * 8.0 * (2.0 * m2 * m1 + m1 * m1 / 2.0),
-        [&] { gprx::launch_gemm(db, g, st); });
+        [&] { gprx::launch_gemm(db, g, st); }, n);
   g.op = gprx::OP_SYRK;
   timed(c, st, "potrf_syrk", Bd * m2 * m2 * m1, Bd * 8.0 * (m2 * m1 + m2 * m2),
-        [&] { gprx::launch_gemm(db, g, st); });
+        [&] { gprx::launch_gemm(db, g, st); }, n);
   factor_rec(c, st, db, o + h, n - h);
   g.op = gprx::OP_TT;
   timed(c, st, "trtri_tt", Bd * m2 * m1 * m1, Bd * 8.0 * (2.0 * m2 * m1 + m1 * m1 / 2.0),
-        [&] { gprx::launch_gemm(db, g, st); });
+        [&] { gprx::launch_gemm(db, g, st); }, n);
   g.op = gprx::OP_LINV21;
   timed(c, st, "trtri_linv21", Bd * m1 * m2 * m2, Bd * 8.0 * (3.0 * m2 * m1 + m2 * m2 / 2.0),
-        [&] { gprx::launch_gemm(db, g, st); });
+        [&] { gprx::launch_gemm(db, g, st); }, n);
 }
 
 void predict_group(gprx_ctx* c, hipStream_t st, const DevBatch& db) {
@@ -324,6 +335,7 @@ int gprx_ctx_create(int device, gprx_ctx** out) {
     return GPRX_DEVICE_ERROR;
   }
   if (const char* ns = getenv("GPRX_STREAMS")) c->nstreams = atoi(ns) > 0 ? atoi(ns) : 1;
+  if (const char* lt = getenv("GPRX_LEAF")) c->leaf_tiles = atoi(lt) >= 1 && atoi(lt) <= 8 ? atoi(lt) : 4;
   c->gstreams.resize(c->nstreams);
   c->gevents.resize(1 + c->nstreams);
   for (auto& st : c->gstreams)
@@ -549,6 +561,10 @@ int gprx_batch_run(gprx_batch* b, const double* theta, unsigned flags, double* m
   {
     const char* ab = getenv("GPRX_ABLATE");  // timing experiments only; results are wrong when set
     db.ablate = ab ? atoi(ab) : 0;
+    const char* gv = getenv("GPRX_GEMMV");
+    db.gemm_variant = gv ? atoi(gv) : 2;
+    const char* lv = getenv("GPRX_LAUUMV");
+    db.lauum_variant = lv ? atoi(lv) : 1;
   }
   const int d = db.d, B = db.B, np = d + 2;
   // hyper-parameters -> kernel parameters, exactly as SEArd / GPE derive them:

@@ -24,6 +24,8 @@ struct DevBatch {
   int M, Mpad, mt;             // test points (per slot), padded to 64, mt = Mpad/64
   int dist_mode;               // GPRX_DIST_EXPANDED / GPRX_DIST_DIRECT
   int ablate;                  // timing-only ablation bits (env GPRX_ABLATE; 0 in production)
+  int gemm_variant;            // k_gemm variant (env GPRX_GEMMV; experiments)
+  int lauum_variant;           // k_lauum_grad variant (env GPRX_LAUUMV; experiments)
   int pst;                     // stride of params per slot
   int gps;                     // stride of per-unit gradient partials (d + 2)
   int ngu;                     // gradient partial units per slot
@@ -70,6 +72,7 @@ struct GemmGeom {
 // kernel launchers (gprx_kernels.hip); every launcher is asynchronous on `s`
 void launch_gram(const DevBatch& b, hipStream_t s);
 void launch_diag(const DevBatch& b, int jt, hipStream_t s);
+void launch_leaf(const DevBatch& b, int o, int n, hipStream_t s);
 void launch_gemm(const DevBatch& b, const GemmGeom& g, hipStream_t s);
 void launch_alpha(const DevBatch& b, hipStream_t s, int phase);
 void launch_lauum_grad(const DevBatch& b, hipStream_t s);

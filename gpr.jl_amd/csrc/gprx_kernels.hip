@@ -90,6 +90,14 @@ __device__ __forceinline__ double sqd2(double a, double a2, double b, double b2,
   return t * t;
 }
 
+// 1/p by v_rcp_f64 + two Newton steps (|error| <= 1 ulp; the reference's dpotf2 scales by 1/ajj too)
+__device__ __forceinline__ double recip(double p) {
+  double r = __builtin_amdgcn_rcp(p);
+  r = fma(r, fma(-p, r, 1.0), r);
+  r = fma(r, fma(-p, r, 1.0), r);
+  return r;
+}
+
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
@@ -107,53 +115,69 @@ __device__ __forceinline__ double wave_sum(double v) {
 //   K is a multiple of 16; operands are prefetched one 16-deep stage ahead into registers.
 // ---------------------------------------------------------------------------------------------
 constexpr int WM = 4, WN = 2;
-__device__ __forceinline__ void mma_64x32(d4 (&acc)[WM][WN], const double* __restrict__ A, size_t lda,
-                                          const double* __restrict__ B, size_t ldb, int K) {
-  if (K <= 0) return;
-  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
-  const double* pa = A + lr + (size_t)lk * lda;
-  const double* pb = B + lr + (size_t)lk * ldb;
-  const size_t sa = 4 * lda, sb = 4 * ldb;
-  double af[4][WM], bf[4][WN];
+struct Frag {
+  double a[4][WM], b[4][WN];
+};
+__device__ __forceinline__ void frag_load(Frag& f, const double* pa, const double* pb, size_t sa, size_t sb) {
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
 #pragma unroll
-    for (int a = 0; a < WM; ++a) af[s][a] = pa[s * sa + 16 * a];
+    for (int a = 0; a < WM; ++a) f.a[s][a] = pa[s * sa + 16 * a];
 #pragma unroll
-    for (int b = 0; b < WN; ++b) bf[s][b] = pb[s * sb + 16 * b];
+    for (int b = 0; b < WN; ++b) f.b[s][b] = pb[s * sb + 16 * b];
   }
-  const int nst = K >> 4;
-  for (int it = 1; it < nst; ++it) {
-    pa += 4 * sa;
-    pb += 4 * sb;
-    double na[4][WM], nb[4][WN];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-#pragma unroll
-      for (int a = 0; a < WM; ++a) na[s][a] = pa[s * sa + 16 * a];
-#pragma unroll
-      for (int b = 0; b < WN; ++b) nb[s][b] = pb[s * sb + 16 * b];
-    }
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-      for (int a = 0; a < WM; ++a)
-#pragma unroll
-        for (int b = 0; b < WN; ++b) acc[a][b] = mfma(bf[s][b], af[s][a], acc[a][b]);
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-#pragma unroll
-      for (int a = 0; a < WM; ++a) af[s][a] = na[s][a];
-#pragma unroll
-      for (int b = 0; b < WN; ++b) bf[s][b] = nb[s][b];
-    }
-  }
+}
+__device__ __forceinline__ void frag_mma(d4 (&acc)[WM][WN], const Frag& f) {
 #pragma unroll
   for (int s = 0; s < 4; ++s)
 #pragma unroll
     for (int a = 0; a < WM; ++a)
 #pragma unroll
-      for (int b = 0; b < WN; ++b) acc[a][b] = mfma(bf[s][b], af[s][a], acc[a][b]);
+      for (int b = 0; b < WN; ++b) acc[a][b] = mfma(f.b[s][b], f.a[s][a], acc[a][b]);
+}
+__device__ __forceinline__ void mma_64x32(d4 (&acc)[WM][WN], const double* __restrict__ A, size_t lda,
+                                          const double* __restrict__ B, size_t ldb, int K) {
+  // K is wave-uniform but derived from threadIdx.x >> 6; make that provable, otherwise hipcc
+  // builds a divergent loop and moves all accumulator registers VGPR<->AGPR every stage.
+  const int nst = __builtin_amdgcn_readfirstlane(K >> 4);
+  if (nst <= 0) return;
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  const double* pa = A + lr + (size_t)lk * lda;
+  const double* pb = B + lr + (size_t)lk * ldb;
+  const size_t sa = 4 * lda, sb = 4 * ldb;
+  // two register stages in ping-pong: stage it+1 is in flight while stage it is multiplied.
+  // K is a multiple of 64 (whole tiles), so nst is even; the last prefetch re-reads the last
+  // stage (clamped index) instead of branching around the loads.
+  Frag f0, f1;
+  frag_load(f0, pa, pb, sa, sb);
+  for (int it = 0; it < nst; it += 2) {
+    frag_load(f1, pa + (size_t)(it + 1) * 4 * sa, pb + (size_t)(it + 1) * 4 * sb, sa, sb);
+    frag_mma(acc, f0);
+    const int n2 = (it + 2 < nst) ? it + 2 : nst - 1;
+    frag_load(f0, pa + (size_t)n2 * 4 * sa, pb + (size_t)n2 * 4 * sb, sa, sb);
+    frag_mma(acc, f1);
+  }
+}
+
+// single register stage (no prefetch): latency is hidden by occupancy instead (4 waves/SIMD)
+__device__ __forceinline__ void mma_64x32_s1(d4 (&acc)[WM][WN], const double* __restrict__ A, size_t lda,
+                                             const double* __restrict__ B, size_t ldb, int K) {
+  const int nst = __builtin_amdgcn_readfirstlane(K >> 4);
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  const double* pa = A + lr + (size_t)lk * lda;
+  const double* pb = B + lr + (size_t)lk * ldb;
+  const size_t sa = 4 * lda, sb = 4 * ldb;
+  for (int it = 0; it < nst; ++it) {
+    Frag f;
+    frag_load(f, pa + (size_t)it * 4 * sa, pb + (size_t)it * 4 * sb, sa, sb);
+    frag_mma(acc, f);
+  }
+}
+template <int V>
+__device__ __forceinline__ void mma_v(d4 (&acc)[WM][WN], const double* __restrict__ A, size_t lda,
+                                      const double* __restrict__ B, size_t ldb, int K) {
+  if constexpr (V == 2) mma_64x32_s1(acc, A, lda, B, ldb, K);
+  else mma_64x32(acc, A, lda, B, ldb, K);
 }
 
 __device__ __forceinline__ void acc_zero(d4 (&acc)[WM][WN]) {
@@ -255,12 +279,14 @@ __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
 // sum_c log L_cc.
 // ============================================================================================
 constexpr int DS = TS + 1;
-__global__ __launch_bounds__(NTHR) void k_diag(DevBatch db, int jt) {
+__device__ __forceinline__ void diag_tile(const DevBatch& db, int slot, int jt) {
   __shared__ double Ls[TS * DS];
   __shared__ double colbuf[2][TS];
   __shared__ double piv[TS];
+  __shared__ double rdiag[TS];
   __shared__ double red[4];
-  const int slot = blockIdx.x, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  __shared__ double rowbuf[2][TS];
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const size_t ld = db.ld;
   const double* A = db.K + (size_t)slot * db.mat + (size_t)jt * TS * ld + jt * TS;
   for (int e = tid; e < TS * TS; e += NTHR) {
@@ -279,20 +305,26 @@ __global__ __launch_bounds__(NTHR) void k_diag(DevBatch db, int jt) {
       for (int q = 0; q < 16; ++q) cb[16 * w + q] = a[q];
     }
     __syncthreads();
+    // all reads of this step issued together, one wait
     const double akk = cb[k];
+    const double ack = cb[lane];
+    double ark[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) ark[q] = cb[16 * w + q];
     const double pk = (akk > 0.0) ? akk : 1.0;
     if (tid == 0) {
       piv[k] = pk;
       if (!(akk > 0.0) && fail < 0) fail = k;
     }
-    const double t = (lane > k) ? cb[lane] / pk : 0.0;
+    const double t = (lane > k) ? ack * recip(pk) : 0.0;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) a[q] = fma(-cb[16 * w + q], t, a[q]);
+    for (int q = 0; q < 16; ++q) a[q] = fma(-ark[q], t, a[q]);
   }
   __syncthreads();
   // L[r][c] = a_rc / sqrt(p_c) (r > c), sqrt(p_c) (r == c), 0 (r < c); into Ls[c][r]
   {
     const double sc = sqrt(piv[lane]), isc = 1.0 / sc;
+    rdiag[lane] = isc;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int r = 16 * w + q;
@@ -315,21 +347,23 @@ __global__ __launch_bounds__(NTHR) void k_diag(DevBatch db, int jt) {
   double x[16];
 #pragma unroll
   for (int q = 0; q < 16; ++q) x[q] = (16 * w + q == lane) ? 1.0 : 0.0;
-  __shared__ double rowbuf[2][TS];
   for (int kb = 0; kb < 4; ++kb) {
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int k = 16 * kb + q;
       double* rb = rowbuf[k & 1];
       if (w == kb) {
-        x[q] = x[q] / Ls[k * DS + k];
+        x[q] = x[q] * rdiag[k];
         rb[lane] = x[q];
       }
       __syncthreads();
       const double xr = rb[lane];
       if (w > kb) {
+        double lk2[16];
 #pragma unroll
-        for (int q2 = 0; q2 < 16; ++q2) x[q2] = fma(-Ls[k * DS + 16 * w + q2], xr, x[q2]);
+        for (int q2 = 0; q2 < 16; ++q2) lk2[q2] = Ls[k * DS + 16 * w + q2];
+#pragma unroll
+        for (int q2 = 0; q2 < 16; ++q2) x[q2] = fma(-lk2[q2], xr, x[q2]);
       } else if (w == kb) {
 #pragma unroll
         for (int q2 = q + 1; q2 < 16; ++q2) x[q2] = fma(-Ls[k * DS + 16 * w + q2], xr, x[q2]);
@@ -348,12 +382,14 @@ __global__ __launch_bounds__(NTHR) void k_diag(DevBatch db, int jt) {
     Mj[(size_t)c * ld + r] = Ls[r * DS + c];  // Mt[r][c]   = X[c][r]
   }
 }
+__global__ __launch_bounds__(NTHR) void k_diag(DevBatch db, int jt) { diag_tile(db, blockIdx.x, jt); }
 
 // ============================================================================================
 // Generic batched tile GEMM of the recursion (see GemmOp).  Unit = pair of vertically adjacent
 // 64x64 output tiles in one tile column; wave (wr, wc) = tile wr of the pair, columns 32wc..+31.
 // ============================================================================================
-__global__ __launch_bounds__(NTHR) void k_gemm(DevBatch db, GemmGeom g) {
+template <int V>
+__device__ __forceinline__ void gemm_body(const DevBatch& db, const GemmGeom& g) {
   const int op = g.op;
   int r0, c0, R, C;
   bool tri = false;
@@ -370,8 +406,13 @@ __global__ __launch_bounds__(NTHR) void k_gemm(DevBatch db, GemmGeom g) {
   if (tri) {
     pair_unit(u, R, C, tri, pr, pc);
   } else {
-    const int P = (R + 1) / 2, pi = u / C;
+    const int P = (R + 1) / 2;
+    int pi = u / C;
     pc = u - pi * C;
+    if (db.ablate & 8) {  // experiment: column-major order (neighbours share the B panel)
+      pc = u / P;
+      pi = u - pc * P;
+    }
     switch (op) {
       case OP_TRSM: pc = C - 1 - pc; pr = 2 * pi; break;      // K grows with the column
       case OP_TT: pr = 2 * pi; break;                           // K shrinks with the row
@@ -400,8 +441,8 @@ __global__ __launch_bounds__(NTHR) void k_gemm(DevBatch db, GemmGeom g) {
   }
   d4 acc[WM][WN];
   acc_zero(acc);
-  mma_64x32(acc, A + (size_t)kb * TS * ld + ti * TS, ld, Bm + (size_t)kb * TS * ldb + tj * TS + 32 * wc, ldb,
-            (ke - kb) * TS);
+  mma_v<V>(acc, A + (size_t)kb * TS * ld + ti * TS, ld, Bm + (size_t)kb * TS * ldb + tj * TS + 32 * wc, ldb,
+           (ke - kb) * TS);
   const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
   if (op == OP_PREDVAR) {
 #pragma unroll
@@ -418,6 +459,15 @@ __global__ __launch_bounds__(NTHR) void k_gemm(DevBatch db, GemmGeom g) {
         if (lr == 0)
           db.var_part[((size_t)slot * db.nt + ti) * db.Mpad + tj * TS + 32 * wc + 16 * b + lk + 4 * q] = v;
       }
+    return;
+  }
+  if (db.ablate & 4) {  // experiment: no epilogue (keep acc live)
+    double t = 0.0;
+#pragma unroll
+    for (int a = 0; a < WM; ++a)
+#pragma unroll
+      for (int b = 0; b < WN; ++b) t += acc[a][b][0] + acc[a][b][3];
+    if (t == 12345.678) db.out[0] = t;
     return;
   }
   double* Cm;
@@ -447,6 +497,109 @@ __global__ __launch_bounds__(NTHR) void k_gemm(DevBatch db, GemmGeom g) {
       for (int b = 0; b < WN; ++b)
 #pragma unroll
         for (int q = 0; q < 4; ++q) Mtt[(size_t)(16 * a + lr) * ld + 16 * b + lk + 4 * q] = -acc[a][b][q];
+  }
+}
+
+__global__ __launch_bounds__(NTHR) void k_gemm(DevBatch db, GemmGeom g) { gemm_body<0>(db, g); }
+__global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_gemm_w3(DevBatch db, GemmGeom g) {
+  gemm_body<0>(db, g);
+}
+__global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_gemm_s1(DevBatch db, GemmGeom g) {
+  gemm_body<2>(db, g);
+}
+
+// ============================================================================================
+// Fused leaf node: Cholesky + inverse of the n <= 4 diagonal tiles o..o+n-1 (a 256x256 block at
+// most) in ONE workgroup per slot, replacing ~4n latency-bound launches of the recursion.
+//   for k: diag(o+k); Lw[i,k] = K[i,k] Linv[k,k]^T (i > k); K[i,j] -= Lw[i,k] Lw[j,k]^T (i >= j > k)
+//   then the off-diagonal inverse tiles by sub-diagonal s = i - j:
+//     X = sum_{t=j}^{i-1} L[i,t] Linv[t,j]  (into Mt[j,i] as scratch),  Linv[i,j] = -Linv[i,i] X
+// Each 64x64 tile task runs on a wave pair (columns 32*half..+31), two tasks at a time.  The X of
+// a task is only re-read by the wave that wrote it (its own 32 columns), so a wave-level fence
+// replaces a barrier between the two products.
+// ============================================================================================
+__device__ __forceinline__ void acc_store(double* C, size_t ld, const d4 (&acc)[WM][WN], double sgn) {
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+#pragma unroll
+  for (int a = 0; a < WM; ++a)
+#pragma unroll
+    for (int b = 0; b < WN; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) C[(size_t)(16 * b + lk + 4 * q) * ld + 16 * a + lr] = sgn * acc[a][b][q];
+}
+__device__ __forceinline__ void acc_sub(double* C, size_t ld, const d4 (&acc)[WM][WN]) {
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+#pragma unroll
+  for (int a = 0; a < WM; ++a)
+#pragma unroll
+    for (int b = 0; b < WN; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        double* p = C + (size_t)(16 * b + lk + 4 * q) * ld + 16 * a + lr;
+        *p = *p - acc[a][b][q];
+      }
+}
+// transposed store: Ct[c][r] = sgn * C[r][c]  (Ct points at the transposed block's origin)
+__device__ __forceinline__ void acc_store_t(double* Ct, size_t ld, const d4 (&acc)[WM][WN], double sgn) {
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+#pragma unroll
+  for (int a = 0; a < WM; ++a)
+#pragma unroll
+    for (int b = 0; b < WN; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Ct[(size_t)(16 * a + lr) * ld + 16 * b + lk + 4 * q] = sgn * acc[a][b][q];
+}
+
+__global__ __launch_bounds__(NTHR) void k_leaf(DevBatch db, int o, int n) {
+  const int slot = blockIdx.x;
+  const int w = threadIdx.x >> 6, half = w & 1, tw = w >> 1;
+  const size_t ld = db.ld, so = (size_t)slot * db.mat;
+  double* K = db.K + so;
+  double* Lw = db.Lw + so;
+  double* Li = db.Linv + so;
+  double* Mt = db.Mt + so;
+  for (int k = 0; k < n; ++k) {
+    const int tk = o + k, m = n - 1 - k;
+    diag_tile(db, slot, tk);
+    __syncthreads();
+    for (int t = tw; t < m; t += 2) {  // TRSM
+      const int ti = tk + 1 + t;
+      d4 acc[WM][WN];
+      acc_zero(acc);
+      mma_64x32(acc, K + (size_t)tk * TS * ld + ti * TS, ld, Li + (size_t)tk * TS * ld + tk * TS + 32 * half, ld, TS);
+      acc_store(Lw + (size_t)(tk * TS + 32 * half) * ld + ti * TS, ld, acc, 1.0);
+    }
+    __syncthreads();
+    for (int t = tw; t < m * (m + 1) / 2; t += 2) {  // SYRK (lower tiles of the trailing block)
+      int a = t, c = 0;
+      while (a >= m - c) {
+        a -= m - c;
+        ++c;
+      }
+      const int tj = tk + 1 + c, ti = tj + a;
+      d4 acc[WM][WN];
+      acc_zero(acc);
+      mma_64x32(acc, Lw + (size_t)tk * TS * ld + ti * TS, ld, Lw + (size_t)tk * TS * ld + tj * TS + 32 * half, ld, TS);
+      acc_sub(K + (size_t)(tj * TS + 32 * half) * ld + ti * TS, ld, acc);
+    }
+    __syncthreads();
+  }
+  for (int s = 1; s < n; ++s) {
+    for (int t = tw; t < n - s; t += 2) {
+      const int tj = o + t, ti = tj + s;
+      double* Xt = Mt + (size_t)(ti * TS) * ld + tj * TS + 32 * half;  // Mt[tj,ti], this wave's rows
+      d4 acc[WM][WN];
+      acc_zero(acc);
+      mma_64x32(acc, Lw + (size_t)tj * TS * ld + ti * TS, ld, Mt + (size_t)tj * TS * ld + tj * TS + 32 * half, ld, s * TS);
+      acc_store_t(Xt, ld, acc, 1.0);
+      __threadfence_block();
+      acc_zero(acc);
+      mma_64x32(acc, Li + (size_t)ti * TS * ld + ti * TS, ld, Xt, ld, TS);
+      __threadfence_block();  // all lanes' reads of X precede the overwrite below
+      acc_store(Li + (size_t)(tj * TS + 32 * half) * ld + ti * TS, ld, acc, -1.0);
+      acc_store_t(Xt, ld, acc, -1.0);
+    }
+    __syncthreads();
   }
 }
 
@@ -487,7 +640,8 @@ __global__ __launch_bounds__(NTHR) void k_alpha(DevBatch db, int phase) {
 // Unit = tile pair (ti, ti+1) x tj of the lower triangle; one gradient partial row per unit.
 // Dynamic LDS: X of the three point tiles [p][64] + their alpha.
 // ============================================================================================
-__global__ __launch_bounds__(NTHR) void k_lauum_grad(DevBatch db) {
+template <int V>
+__device__ __forceinline__ void lauum_body(const DevBatch& db) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int d = db.d, tid = threadIdx.x, w = tid >> 6, wr = w >> 1, wc = w & 1;
   double* xr_s = sm;                // [2][d][64] rows of ti, ti+1
@@ -522,8 +676,8 @@ __global__ __launch_bounds__(NTHR) void k_lauum_grad(DevBatch db) {
   acc_zero(acc);
   const size_t ld = db.ld, so = (size_t)slot * db.mat;
   if (active && !(db.ablate & 1))
-    mma_64x32(acc, db.Mt + so + (size_t)ti * TS * ld + ti * TS, ld, db.Mt + so + (size_t)ti * TS * ld + tj * TS + 32 * wc,
-              ld, (nt - ti) * TS);
+    mma_v<V>(acc, db.Mt + so + (size_t)ti * TS * ld + ti * TS, ld, db.Mt + so + (size_t)ti * TS * ld + tj * TS + 32 * wc,
+             ld, (nt - ti) * TS);
   __syncthreads();
   double sf = 0.0, tr = 0.0;
   const double* xr = xr_s + wr * d * TS;
@@ -590,6 +744,13 @@ __global__ __launch_bounds__(NTHR) void k_lauum_grad(DevBatch db) {
   double* out = db.grad_part + ((size_t)slot * db.ngu + u) * db.gps;
   for (int e = tid; e < d + 2; e += NTHR)
     out[e] = ((sp[e] + sp[(DMAX + 2) + e]) + sp[2 * (DMAX + 2) + e]) + sp[3 * (DMAX + 2) + e];
+}
+__global__ __launch_bounds__(NTHR) void k_lauum_grad(DevBatch db) { lauum_body<0>(db); }
+__global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_lauum_grad_w3(DevBatch db) {
+  lauum_body<0>(db);
+}
+__global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_lauum_grad_s1(DevBatch db) {
+  lauum_body<2>(db);
 }
 int lauum_units(int nt) { return pair_units(nt, nt, true); }
 void lauum_order_host(int nt, int* out) {
@@ -759,7 +920,8 @@ static void set_lds_limits() {
   if (done) return;
   done = true;
   (void)hipFuncSetAttribute((const void*)k_gram, hipFuncAttributeMaxDynamicSharedMemorySize, (int)gram_lds(DMAX));
-  (void)hipFuncSetAttribute((const void*)k_lauum_grad, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lauum_lds(DMAX));
+  for (const void* f : {(const void*)k_lauum_grad, (const void*)k_lauum_grad_w3, (const void*)k_lauum_grad_s1})
+    (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lauum_lds(DMAX));
   (void)hipFuncSetAttribute((const void*)k_pred_cross, hipFuncAttributeMaxDynamicSharedMemorySize, (int)cross_lds(DMAX));
 }
 
@@ -769,6 +931,9 @@ void launch_gram(const DevBatch& b, hipStream_t s) {
 }
 void launch_diag(const DevBatch& b, int jt, hipStream_t s) {
   hipLaunchKernelGGL(k_diag, dim3(b.B), dim3(NTHR), 0, s, b, jt);
+}
+void launch_leaf(const DevBatch& b, int o, int n, hipStream_t s) {
+  hipLaunchKernelGGL(k_leaf, dim3(b.B), dim3(NTHR), 0, s, b, o, n);
 }
 void launch_gemm(const DevBatch& b, const GemmGeom& g, hipStream_t s) {
   int R, C;
@@ -780,14 +945,24 @@ void launch_gemm(const DevBatch& b, const GemmGeom& g, hipStream_t s) {
     case OP_TT: R = g.h; C = g.n - g.h; break;
     default: R = b.nt; C = b.mt; break;
   }
-  hipLaunchKernelGGL(k_gemm, dim3(grid_blocks(b.B, pair_units(R, C, tri))), dim3(NTHR), 0, s, b, g);
+  const dim3 grid(grid_blocks(b.B, pair_units(R, C, tri)));
+  switch (b.gemm_variant) {
+    case 1: hipLaunchKernelGGL(k_gemm_w3, grid, dim3(NTHR), 0, s, b, g); break;
+    case 2: hipLaunchKernelGGL(k_gemm_s1, grid, dim3(NTHR), 0, s, b, g); break;
+    default: hipLaunchKernelGGL(k_gemm, grid, dim3(NTHR), 0, s, b, g); break;
+  }
 }
 void launch_alpha(const DevBatch& b, hipStream_t s, int phase) {
   hipLaunchKernelGGL(k_alpha, dim3(grid_blocks(b.B, b.nt)), dim3(NTHR), 0, s, b, phase);
 }
 void launch_lauum_grad(const DevBatch& b, hipStream_t s) {
   set_lds_limits();
-  hipLaunchKernelGGL(k_lauum_grad, dim3(grid_blocks(b.B, lauum_units(b.nt))), dim3(NTHR), lauum_lds(b.d), s, b);
+  const dim3 grid(grid_blocks(b.B, lauum_units(b.nt)));
+  switch (b.lauum_variant) {
+    case 1: hipLaunchKernelGGL(k_lauum_grad_w3, grid, dim3(NTHR), lauum_lds(b.d), s, b); break;
+    case 2: hipLaunchKernelGGL(k_lauum_grad_s1, grid, dim3(NTHR), lauum_lds(b.d), s, b); break;
+    default: hipLaunchKernelGGL(k_lauum_grad, grid, dim3(NTHR), lauum_lds(b.d), s, b); break;
+  }
 }
 void launch_finalize(const DevBatch& b, int want_grad, hipStream_t s) {
   hipLaunchKernelGGL(k_finalize, dim3(b.B), dim3(NTHR), 0, s, b, want_grad);
