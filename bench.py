@@ -55,7 +55,32 @@ def make_workload(trials_per_gpu: int, rank: int, world: int, seed_base: int = 0
     return np.stack(Xs), np.stack(Ys), np.stack(Ts), np.stack(XTs)
 
 
-def cpu_baseline(X, Y, T, XT, max_seconds: float = 20.0, max_fits: int = 3):
+# library stat name -> kernel symbol (prefix) in rocprofv3 output; k_gemm serves several stats
+SYMBOL = {"gram": "k_gram", "leaf": "k_leaf", "diag": "k_diag", "alpha": "k_alpha", "lauum_grad": "k_lauum_grad",
+          "finalize": "k_finalize", "pred_cross": "k_pred_cross", "pred_final": "k_pred_final"}
+
+
+def pmc_traffic(stat: str, global_batch: int):
+    """HBM bytes per launch of `stat`'s kernel from the committed PMC summary (profiles/collect.sh),
+    if it was collected on this same workload; else None."""
+    f = REPO / "profiles" / "pmc_latest.json"
+    sym = SYMBOL.get(stat)
+    if sym is None or not f.exists():
+        return None
+    try:
+        s = json.loads(f.read_text())
+        if (s.get("bench_under_rocprof") or {}).get("config", {}).get("global_batch") != global_batch:
+            return None
+        for k, e in s["kernels"].items():
+            if k.startswith(sym) and "traffic_bytes_per_launch" in e:
+                return {"bytes_per_launch": e["traffic_bytes_per_launch"], "source": f"profiles/{s['round']}_summary.json",
+                        "kernel_symbol": k}
+    except Exception:
+        return None
+    return None
+
+
+def cpu_baseline(X, Y, T, XT, max_seconds: float = 15.0, max_fits: int = 32):
     """Oracle (CPU restatement, numpy + OpenBLAS LAPACK) on a bounded sample of the same workload."""
     sys.path.insert(0, str(REPO))
     from oracle import gp_oracle as O
@@ -85,7 +110,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--trials", type=int, default=int(os.environ.get("GPRX_BENCH_TRIALS", "8")),
+    ap.add_argument("--trials", type=int, default=int(os.environ.get("GPRX_BENCH_TRIALS", "32")),
                     help="P2 trials per GPU per step (x6 output GPs)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-prof", action="store_true")
@@ -147,7 +172,7 @@ def main():
         for _ in range(nprof):
             batch.run(T, grad=True, predict=True)
         ctx.set_profiling(False)
-        names = ["gram", "diag", "potrf_trsm", "potrf_syrk", "trtri_tt", "trtri_linv21", "alpha", "lauum_grad",
+        names = ["gram", "leaf", "diag", "potrf_trsm", "potrf_syrk", "trtri_tt", "syrk_tt", "trtri_linv21", "alpha", "lauum_grad",
                  "finalize", "pred_cross", "pred_var", "pred_final"]
         for nme in names:
             kern[nme] = ctx.kernel_stats(nme)
@@ -156,8 +181,13 @@ def main():
         avg_ms = s["ms"] / max(1, s["launches"])
         per_launch_flops = s["flops"] / max(1, s["launches"])
         achieved = per_launch_flops / (avg_ms * 1e-3) / 1e12
+        tr = pmc_traffic(dom, B * world)
         roof = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 3), "peak": PEAK_FP64_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP64_TFLOPS, 4), "traffic": None,
+                "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP64_TFLOPS, 4),
+                "traffic": round(tr["bytes_per_launch"]) if tr else None,
+                "traffic_unit": "bytes/launch (PMC 2*FETCH_SIZE+WRITE_SIZE)", "traffic_source": tr,
+                "algorithmic_bytes_per_launch": round(s["bytes"] / max(1, s["launches"])),
+                "algorithmic_flops_per_launch": per_launch_flops,
                 "avg_launch_ms": round(avg_ms, 4), "launches_per_step": s["launches"] // nprof}
     step_flops = B * fit_flops(N, d, M)
     cpu = None

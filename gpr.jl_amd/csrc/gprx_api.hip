@@ -43,6 +43,7 @@ struct gprx_ctx {
   std::vector<PendingEv> pending;
   int nstreams = 1;                   // slot groups run concurrently on these streams (1: measured best)
   int leaf_tiles = 4;                 // recursion nodes of <= this many tiles run fused (k_leaf)
+  bool fuse_tt = true;                // TT shares the SYRK launch (env GPRX_FUSE_TT=0 to split)
   std::vector<hipStream_t> gstreams;  // group streams
   std::vector<hipEvent_t> gevents;    // fork/join events (1 + nstreams)
 };
@@ -242,18 +243,23 @@ void factor_rec(gprx_ctx* c, hipStream_t st, const DevBatch& db, int o, int n) {
   const double m1 = h * T, m2 = (n - h) * T;
   factor_rec(c, st, db, o, h);
   gprx::GemmGeom g{gprx::OP_TRSM, o, h, n};
-  timed(c, st, "potrf_trsm", Bd * m2 * m1 * m1, Bd * 8.0 * (2.0 * m2 * m1 + m1 * m1 / 2.0),
-        [&] { gprx::launch_gemm(db, g, st); }, n);
-  g.op = gprx::OP_SYRK;
-  timed(c, st, "potrf_syrk", Bd * m2 * m2 * m1, Bd * 8.0 * (m2 * m1 + m2 * m2),
-        [&] { gprx::launch_gemm(db, g, st); }, n);
-  factor_rec(c, st, db, o + h, n - h);
-  g.op = gprx::OP_TT;
-  timed(c, st, "trtri_tt", Bd * m2 * m1 * m1, Bd * 8.0 * (2.0 * m2 * m1 + m1 * m1 / 2.0),
-        [&] { gprx::launch_gemm(db, g, st); }, n);
+  const double f_trsm = Bd * m2 * m1 * m1, f_syrk = Bd * m2 * m2 * m1, f_tt = Bd * m2 * m1 * m1,
+               f_linv = Bd * m1 * m2 * m2;
+  const double b_trsm = Bd * 8.0 * (2.0 * m2 * m1 + m1 * m1 / 2.0), b_syrk = Bd * 8.0 * (m2 * m1 + m2 * m2),
+               b_tt = Bd * 8.0 * (2.0 * m2 * m1 + m1 * m1 / 2.0), b_linv = Bd * 8.0 * (3.0 * m2 * m1 + m2 * m2 / 2.0);
+  timed(c, st, "potrf_trsm", f_trsm, b_trsm, [&] { gprx::launch_gemm(db, g, st); }, n);
+  gprx::GemmGeom gs{gprx::OP_SYRK, o, h, n}, gt{gprx::OP_TT, o, h, n};
+  if (c->fuse_tt) {
+    // T^T = L11^-T L21^T needs only rec(A11) and the TRSM: it runs in the SYRK's launch
+    timed(c, st, "syrk_tt", f_syrk + f_tt, b_syrk + b_tt, [&] { gprx::launch_gemm(db, gs, st, gt); }, n);
+    factor_rec(c, st, db, o + h, n - h);
+  } else {
+    timed(c, st, "potrf_syrk", f_syrk, b_syrk, [&] { gprx::launch_gemm(db, gs, st); }, n);
+    factor_rec(c, st, db, o + h, n - h);
+    timed(c, st, "trtri_tt", f_tt, b_tt, [&] { gprx::launch_gemm(db, gt, st); }, n);
+  }
   g.op = gprx::OP_LINV21;
-  timed(c, st, "trtri_linv21", Bd * m1 * m2 * m2, Bd * 8.0 * (3.0 * m2 * m1 + m2 * m2 / 2.0),
-        [&] { gprx::launch_gemm(db, g, st); }, n);
+  timed(c, st, "trtri_linv21", f_linv, b_linv, [&] { gprx::launch_gemm(db, g, st); }, n);
 }
 
 void predict_group(gprx_ctx* c, hipStream_t st, const DevBatch& db) {
@@ -335,6 +341,7 @@ int gprx_ctx_create(int device, gprx_ctx** out) {
     return GPRX_DEVICE_ERROR;
   }
   if (const char* ns = getenv("GPRX_STREAMS")) c->nstreams = atoi(ns) > 0 ? atoi(ns) : 1;
+  if (const char* ft = getenv("GPRX_FUSE_TT")) c->fuse_tt = atoi(ft) != 0;
   if (const char* lt = getenv("GPRX_LEAF")) c->leaf_tiles = atoi(lt) >= 1 && atoi(lt) <= 8 ? atoi(lt) : 4;
   c->gstreams.resize(c->nstreams);
   c->gevents.resize(1 + c->nstreams);

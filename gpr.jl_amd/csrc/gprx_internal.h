@@ -64,16 +64,30 @@ enum GemmOp : int {
   OP_LINV21 = 3,  // Linv[b2,b1] = -Linv[b2,b2] T ; Mt[b1,b2] = Linv[b2,b1]^T
   OP_PREDVAR = 4  // var_part   = colsum((Linv K*)^2)
 };
+constexpr int OP_NONE = -1;
 struct GemmGeom {
   int op;
   int o, h, n;  // node: offset o, split h, size n (tile units); block1 = [o, o+h), block2 = [o+h, o+n)
 };
+// Output rectangle of an op in tiles: origin (r0, c0), R x C, lower triangle only when tri.
+__host__ __device__ inline void op_rect(const GemmGeom& g, int nt, int mt, int& r0, int& c0, int& R, int& C, bool& tri) {
+  tri = false;
+  switch (g.op) {
+    case OP_TRSM:
+    case OP_LINV21: r0 = g.o + g.h; c0 = g.o; R = g.n - g.h; C = g.h; break;
+    case OP_SYRK: r0 = c0 = g.o + g.h; R = C = g.n - g.h; tri = true; break;
+    case OP_TT: r0 = g.o; c0 = g.o + g.h; R = g.h; C = g.n - g.h; break;
+    case OP_PREDVAR: r0 = 0; c0 = 0; R = nt; C = mt; break;
+    default: r0 = c0 = R = C = 0; break;
+  }
+}
 
 // kernel launchers (gprx_kernels.hip); every launcher is asynchronous on `s`
 void launch_gram(const DevBatch& b, hipStream_t s);
 void launch_diag(const DevBatch& b, int jt, hipStream_t s);
 void launch_leaf(const DevBatch& b, int o, int n, hipStream_t s);
-void launch_gemm(const DevBatch& b, const GemmGeom& g, hipStream_t s);
+// one launch; with g2.op != OP_NONE the units of g2 are appended to g's (independent ops)
+void launch_gemm(const DevBatch& b, const GemmGeom& g, hipStream_t s, const GemmGeom& g2 = GemmGeom{OP_NONE, 0, 0, 0});
 void launch_alpha(const DevBatch& b, hipStream_t s, int phase);
 void launch_lauum_grad(const DevBatch& b, hipStream_t s);
 int lauum_units(int nt);

@@ -389,30 +389,27 @@ __global__ __launch_bounds__(NTHR) void k_diag(DevBatch db, int jt) { diag_tile(
 // 64x64 output tiles in one tile column; wave (wr, wc) = tile wr of the pair, columns 32wc..+31.
 // ============================================================================================
 template <int V>
-__device__ __forceinline__ void gemm_body(const DevBatch& db, const GemmGeom& g) {
-  const int op = g.op;
-  int r0, c0, R, C;
-  bool tri = false;
-  switch (op) {
-    case OP_TRSM:
-    case OP_LINV21: r0 = g.o + g.h; c0 = g.o; R = g.n - g.h; C = g.h; break;
-    case OP_SYRK: r0 = c0 = g.o + g.h; R = C = g.n - g.h; tri = true; break;
-    case OP_TT: r0 = g.o; c0 = g.o + g.h; R = g.h; C = g.n - g.h; break;
-    default: r0 = 0; c0 = 0; R = db.nt; C = db.mt; break;  // OP_PREDVAR
-  }
+__device__ __forceinline__ void gemm_body(const DevBatch& db, const GemmGeom& g1, const GemmGeom& g2) {
+  int r0, c0, R, C, r02, c02, R2, C2;
+  bool tri, tri2;
+  op_rect(g1, db.nt, db.mt, r0, c0, R, C, tri);
+  op_rect(g2, db.nt, db.mt, r02, c02, R2, C2, tri2);
+  const int T1 = pair_units(R, C, tri), T2 = g2.op == OP_NONE ? 0 : pair_units(R2, C2, tri2);
   int slot, u, pr, pc;
-  if (!map_block(blockIdx.x, db.B, pair_units(R, C, tri), slot, u)) return;
+  if (!map_block(blockIdx.x, db.B, T1 + T2, slot, u)) return;
+  const GemmGeom g = u < T1 ? g1 : g2;  // block-uniform
+  if (u >= T1) {
+    u -= T1;
+    r0 = r02; c0 = c02; R = R2; C = C2; tri = tri2;
+  }
+  const int op = g.op;
   // longest K range first (the tail of a launch is its longest units)
   if (tri) {
     pair_unit(u, R, C, tri, pr, pc);
   } else {
     const int P = (R + 1) / 2;
-    int pi = u / C;
+    const int pi = u / C;
     pc = u - pi * C;
-    if (db.ablate & 8) {  // experiment: column-major order (neighbours share the B panel)
-      pc = u / P;
-      pi = u - pc * P;
-    }
     switch (op) {
       case OP_TRSM: pc = C - 1 - pc; pr = 2 * pi; break;      // K grows with the column
       case OP_TT: pr = 2 * pi; break;                           // K shrinks with the row
@@ -500,12 +497,14 @@ __device__ __forceinline__ void gemm_body(const DevBatch& db, const GemmGeom& g)
   }
 }
 
-__global__ __launch_bounds__(NTHR) void k_gemm(DevBatch db, GemmGeom g) { gemm_body<0>(db, g); }
-__global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_gemm_w3(DevBatch db, GemmGeom g) {
-  gemm_body<0>(db, g);
+__global__ __launch_bounds__(NTHR) void k_gemm(DevBatch db, GemmGeom g, GemmGeom g2) { gemm_body<0>(db, g, g2); }
+__global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_gemm_w3(DevBatch db, GemmGeom g,
+                                                                                            GemmGeom g2) {
+  gemm_body<0>(db, g, g2);
 }
-__global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_gemm_s1(DevBatch db, GemmGeom g) {
-  gemm_body<2>(db, g);
+__global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_gemm_s1(DevBatch db, GemmGeom g,
+                                                                                            GemmGeom g2) {
+  gemm_body<2>(db, g, g2);
 }
 
 // ============================================================================================
@@ -935,21 +934,20 @@ void launch_diag(const DevBatch& b, int jt, hipStream_t s) {
 void launch_leaf(const DevBatch& b, int o, int n, hipStream_t s) {
   hipLaunchKernelGGL(k_leaf, dim3(b.B), dim3(NTHR), 0, s, b, o, n);
 }
-void launch_gemm(const DevBatch& b, const GemmGeom& g, hipStream_t s) {
-  int R, C;
-  bool tri = false;
-  switch (g.op) {
-    case OP_TRSM:
-    case OP_LINV21: R = g.n - g.h; C = g.h; break;
-    case OP_SYRK: R = C = g.n - g.h; tri = true; break;
-    case OP_TT: R = g.h; C = g.n - g.h; break;
-    default: R = b.nt; C = b.mt; break;
+void launch_gemm(const DevBatch& b, const GemmGeom& g, hipStream_t s, const GemmGeom& g2) {
+  int r0, c0, R, C;
+  bool tri;
+  op_rect(g, b.nt, b.mt, r0, c0, R, C, tri);
+  int T = pair_units(R, C, tri);
+  if (g2.op != OP_NONE) {
+    op_rect(g2, b.nt, b.mt, r0, c0, R, C, tri);
+    T += pair_units(R, C, tri);
   }
-  const dim3 grid(grid_blocks(b.B, pair_units(R, C, tri)));
+  const dim3 grid(grid_blocks(b.B, T));
   switch (b.gemm_variant) {
-    case 1: hipLaunchKernelGGL(k_gemm_w3, grid, dim3(NTHR), 0, s, b, g); break;
-    case 2: hipLaunchKernelGGL(k_gemm_s1, grid, dim3(NTHR), 0, s, b, g); break;
-    default: hipLaunchKernelGGL(k_gemm, grid, dim3(NTHR), 0, s, b, g); break;
+    case 1: hipLaunchKernelGGL(k_gemm_w3, grid, dim3(NTHR), 0, s, b, g, g2); break;
+    case 2: hipLaunchKernelGGL(k_gemm_s1, grid, dim3(NTHR), 0, s, b, g, g2); break;
+    default: hipLaunchKernelGGL(k_gemm, grid, dim3(NTHR), 0, s, b, g, g2); break;
   }
 }
 void launch_alpha(const DevBatch& b, hipStream_t s, int phase) {
