@@ -44,6 +44,9 @@ struct gprx_ctx {
   int nstreams = 1;                   // slot groups run concurrently on these streams (1: measured best)
   int leaf_tiles = 4;                 // recursion nodes of <= this many tiles run fused (k_leaf)
   bool fuse_tt = true;                // TT shares the SYRK launch (env GPRX_FUSE_TT=0 to split)
+  // replay each batch's launch sequence as a hipGraph (GPRX_GRAPHS=1).  Off by default: measured
+  // equal to direct launches at B=1..192 (the launches are queued far ahead of the GPU).
+  bool use_graphs = false;
   std::vector<hipStream_t> gstreams;  // group streams
   std::vector<hipEvent_t> gevents;    // fork/join events (1 + nstreams)
 };
@@ -60,6 +63,11 @@ struct gprx_batch {
   bool factored = false;
   bool have_train = false;
   bool have_test = false;
+  // captured evaluation graphs, one per (want_grad, want_pred); valid while the key matches
+  hipGraphExec_t gexec[4] = {};
+  DevBatch gkey[4];
+  int gkey_ctx[4][2] = {};
+  bool gvalid[4] = {};
 };
 
 struct gprx_gp {
@@ -289,6 +297,39 @@ void eval_group(gprx_ctx* c, hipStream_t st, const DevBatch& db, bool want_grad,
 }
 
 // Fork the slot groups of `b` over the context's group streams, join back on the main stream.
+// One evaluation as a replayed hipGraph: ~40-50 dependent launches per evaluation become one
+// graph launch (captured on first use; re-captured when the batch geometry, the test set or a
+// kernel variant changes).  Used when profiling is off and the batch is one slot group.
+int run_graph(gprx_batch* b, bool want_grad, bool want_pred) {
+  gprx_ctx* c = b->ctx;
+  const DevBatch& db = b->db;
+  const int gi = (want_grad ? 1 : 0) + (want_pred ? 2 : 0);
+  const bool same = b->gvalid[gi] && memcmp(&b->gkey[gi], &db, sizeof(DevBatch)) == 0 &&
+                    b->gkey_ctx[gi][0] == c->leaf_tiles && b->gkey_ctx[gi][1] == (int)c->fuse_tt;
+  if (!same) {
+    if (b->gvalid[gi]) (void)hipGraphExecDestroy(b->gexec[gi]);
+    b->gvalid[gi] = false;
+    hipGraph_t graph = nullptr;
+    HIPCHK(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+    eval_group(c, c->stream, db, want_grad, want_pred);
+    const hipError_t le = hipGetLastError();
+    const hipError_t ce = hipStreamEndCapture(c->stream, &graph);
+    if (le != hipSuccess || ce != hipSuccess) {
+      if (graph) (void)hipGraphDestroy(graph);
+      return set_err(c, GPRX_DEVICE_ERROR, std::string("graph capture: ") + hipGetErrorString(le != hipSuccess ? le : ce));
+    }
+    const hipError_t ie = hipGraphInstantiate(&b->gexec[gi], graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    HIPCHK(c, ie);
+    memcpy(&b->gkey[gi], &db, sizeof(DevBatch));
+    b->gkey_ctx[gi][0] = c->leaf_tiles;
+    b->gkey_ctx[gi][1] = (int)c->fuse_tt;
+    b->gvalid[gi] = true;
+  }
+  HIPCHK(c, hipGraphLaunch(b->gexec[gi], c->stream));
+  return GPRX_OK;
+}
+
 int run_groups(gprx_batch* b, bool want_grad, bool want_pred, bool factor) {
   gprx_ctx* c = b->ctx;
   const DevBatch& db = b->db;
@@ -342,6 +383,7 @@ int gprx_ctx_create(int device, gprx_ctx** out) {
   }
   if (const char* ns = getenv("GPRX_STREAMS")) c->nstreams = atoi(ns) > 0 ? atoi(ns) : 1;
   if (const char* ft = getenv("GPRX_FUSE_TT")) c->fuse_tt = atoi(ft) != 0;
+  if (const char* gr = getenv("GPRX_GRAPHS")) c->use_graphs = atoi(gr) != 0;
   if (const char* lt = getenv("GPRX_LEAF")) c->leaf_tiles = atoi(lt) >= 1 && atoi(lt) <= 8 ? atoi(lt) : 4;
   c->gstreams.resize(c->nstreams);
   c->gevents.resize(1 + c->nstreams);
@@ -478,6 +520,8 @@ void gprx_batch_destroy(gprx_batch* b) {
   if (!b) return;
   if (b->ctx) (void)hipSetDevice(b->ctx->device);
   if (b->ctx) (void)hipStreamSynchronize(b->ctx->stream);
+  for (int i = 0; i < 4; ++i)
+    if (b->gvalid[i]) (void)hipGraphExecDestroy(b->gexec[i]);
   for (void* p : b->allocs) (void)hipFree(p);
   if (b->h_params) (void)hipHostFree(b->h_params);
   if (b->h_out) (void)hipHostFree(b->h_out);
@@ -570,6 +614,12 @@ int gprx_batch_run(gprx_batch* b, const double* theta, unsigned flags, double* m
     db.ablate = ab ? atoi(ab) : 0;
     const char* gv = getenv("GPRX_GEMMV");
     db.gemm_variant = gv ? atoi(gv) : 2;
+    const char* gvs = getenv("GPRX_GEMMV_SMALL");
+    db.gemm_variant_small = gvs ? atoi(gvs) : db.gemm_variant;
+    const char* sn = getenv("GPRX_SMALL_N");
+    db.small_n = sn ? atoi(sn) : 8;
+    const char* dv = getenv("GPRX_DIAGV");
+    db.diag_variant = dv ? atoi(dv) : 1;
     const char* lv = getenv("GPRX_LAUUMV");
     db.lauum_variant = lv ? atoi(lv) : 1;
   }
@@ -595,7 +645,8 @@ int gprx_batch_run(gprx_batch* b, const double* theta, unsigned flags, double* m
   const bool want_grad = (flags & GPRX_WANT_GRAD) != 0;
   const bool want_pred = (flags & GPRX_WANT_PREDICT) != 0 && b->have_test && db.M > 0;
   {
-    int rc = run_groups(b, want_grad, want_pred, true);
+    const bool graph = c->use_graphs && !c->prof && n_groups(c, B) == 1;
+    int rc = graph ? run_graph(b, want_grad, want_pred) : run_groups(b, want_grad, want_pred, true);
     if (rc) return rc;
   }
   HIPCHK(c, hipMemcpyAsync(b->h_out, db.out, (size_t)B * (d + 3) * sizeof(double), hipMemcpyDeviceToHost, c->stream));

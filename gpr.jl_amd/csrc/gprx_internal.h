@@ -25,7 +25,10 @@ struct DevBatch {
   int dist_mode;               // GPRX_DIST_EXPANDED / GPRX_DIST_DIRECT
   int ablate;                  // timing-only ablation bits (env GPRX_ABLATE; 0 in production)
   int gemm_variant;            // k_gemm variant (env GPRX_GEMMV; experiments)
+  int gemm_variant_small;      // variant for recursion nodes of <= small_n tiles (GPRX_GEMMV_SMALL)
+  int small_n;                 // (GPRX_SMALL_N)
   int lauum_variant;           // k_lauum_grad variant (env GPRX_LAUUMV; experiments)
+  int diag_variant;            // 0: 4-wave k_diag, 1: one-wave k_diag_w (env GPRX_DIAGV)
   int pst;                     // stride of params per slot
   int gps;                     // stride of per-unit gradient partials (d + 2)
   int ngu;                     // gradient partial units per slot

@@ -384,6 +384,148 @@ __device__ __forceinline__ void diag_tile(const DevBatch& db, int slot, int jt) 
 }
 __global__ __launch_bounds__(NTHR) void k_diag(DevBatch db, int jt) { diag_tile(db, blockIdx.x, jt); }
 
+// --------------------------------------------------------------------------------------------
+// Same leaf, ONE wave per slot (no workgroup barriers on the 128-step dependency chain).
+//   Cholesky: lane = row r; the row's not-yet-final columns sit in registers as chunks of 16,
+//     the current block's chunk first (chunks shift down after each block of 16 steps, so every
+//     register index is static).  Step k broadcasts the pivot a_kk by readlane, scales the column
+//     (l_rk = a_rk / l_kk), publishes it through LDS (col[k][r] = l_rk, 0 for r <= k) and updates
+//     a_rc -= l_rk l_ck for all remaining columns (zeros make c <= k a no-op).
+//   Inverse: lane = column c of X = L^-1, forward substitution by columns of L read back from
+//     the LDS image (x_k *= 1/l_kk ; x_r -= l_rk x_k), finished rows parked in an LDS tile T.
+//   Outputs from T: Mt (lanes = columns of Mt, contiguous) and Linv (lanes = rows).
+//   Pivot failure handled as in k_diag.  LDS: DWS doubles per wave.
+// --------------------------------------------------------------------------------------------
+constexpr int CS = 66;  // LDS row stride (16-B aligned rows)
+constexpr int DWS = 2 * TS * CS;
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, lane);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+// a[q][i] -= f * v[16q + i] for the NQ live chunks (static), 8 columns at a time
+template <int NQ>
+__device__ __forceinline__ void chunk_update(double (&a)[4][16], const double* v, double f) {
+#pragma unroll
+  for (int q = 0; q < NQ; ++q)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      double2 b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) b[i] = *(const double2*)(v + 16 * q + 8 * h + 2 * i);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        a[q][8 * h + 2 * i] = fma(-f, b[i].x, a[q][8 * h + 2 * i]);
+        a[q][8 * h + 2 * i + 1] = fma(-f, b[i].y, a[q][8 * h + 2 * i + 1]);
+      }
+    }
+}
+// 16 Cholesky steps of block kb (NQ = 4 - kb live chunks)
+template <int NQ>
+__device__ __forceinline__ void potrf_block(double (&a)[4][16], double* col, int kb, int r, int& fail) {
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int k = 16 * kb + j;
+    const double ak = a[0][j];
+    const double p = readlane_d(ak, k);
+    const double pk = (p > 0.0) ? p : 1.0;
+    if (!(p > 0.0) && fail < 0) fail = k;
+    const double lkk = sqrt(pk), rk = recip(lkk);
+    const double l = (r > k) ? ak * rk : 0.0;
+    // column k of L below the diagonal; 1/l_kk parked on the diagonal (no lane branch: a
+    // branch here splits the block and lets the compiler sink the FMAs across steps)
+    col[k * CS + r] = (r == k) ? rk : l;
+    __builtin_amdgcn_wave_barrier();
+    chunk_update<NQ>(a, col + k * CS + 16 * kb, l);
+    // keep each step's reads and FMAs inside the step: otherwise the scheduler defers the FMAs
+    // of far columns behind the pivot chain and spills the early-issued LDS reads
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+template <int NQ>
+__device__ __forceinline__ void trtri_block(double (&a)[4][16], const double* col, int kb) {
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int k = 16 * kb + j;
+    const double* ck = col + k * CS;
+    const double xk = a[0][j] * ck[k];
+    chunk_update<NQ>(a, ck + 16 * kb, xk);  // l_rk for r > k, 0 for r < k (r = k: restored below)
+    a[0][j] = xk;
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+__device__ __forceinline__ void chunk_shift(double (&a)[4][16]) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    a[0][i] = a[1][i];
+    a[1][i] = a[2][i];
+    a[2][i] = a[3][i];
+  }
+}
+__device__ __forceinline__ void diag_wave(const DevBatch& db, int slot, int jt, double* sm) {
+  const int r = threadIdx.x & 63;
+  const size_t ld = db.ld;
+  double* col = sm;               // [64][CS]: column k of L at col[k*CS + r]
+  double* T = sm + TS * CS;       // [64][CS]: X rows
+  const double* A = db.K + (size_t)slot * db.mat + (size_t)jt * TS * ld + jt * TS;
+  double a[4][16];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) a[q][i] = A[(size_t)(16 * q + i) * ld + r];  // lower part used only
+  int fail = -1;
+  potrf_block<4>(a, col, 0, r, fail);
+  chunk_shift(a);
+  potrf_block<3>(a, col, 1, r, fail);
+  chunk_shift(a);
+  potrf_block<2>(a, col, 2, r, fail);
+  chunk_shift(a);
+  potrf_block<1>(a, col, 3, r, fail);
+  __builtin_amdgcn_wave_barrier();
+  {
+    const double s = -wave_sum(log(col[r * CS + r]));  // sum log l_kk = -sum log(1/l_kk)
+    if (r == 0) {
+      db.logdet_part[(size_t)slot * db.nt + jt] = s;
+      if (fail >= 0 && db.status[slot] == 0) {
+        db.status[slot] = 1;
+        db.info[slot] = jt * TS + fail + 1;
+      }
+    }
+  }
+  // X = L^-1, lane = column c
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) a[q][i] = (16 * q + i == r) ? 1.0 : 0.0;
+  trtri_block<4>(a, col, 0);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) T[i * CS + r] = a[0][i];  // X[i][c], lane c
+  chunk_shift(a);
+  trtri_block<3>(a, col, 1);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) T[(16 + i) * CS + r] = a[0][i];
+  chunk_shift(a);
+  trtri_block<2>(a, col, 2);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) T[(32 + i) * CS + r] = a[0][i];
+  chunk_shift(a);
+  trtri_block<1>(a, col, 3);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) T[(48 + i) * CS + r] = a[0][i];
+  __builtin_amdgcn_wave_barrier();
+  double* Mj = db.Mt + (size_t)slot * db.mat + (size_t)jt * TS * ld + jt * TS;
+  double* Li = db.Linv + (size_t)slot * db.mat + (size_t)jt * TS * ld + jt * TS;
+  for (int q = 0; q < TS; ++q) {
+    Mj[(size_t)q * ld + r] = T[q * CS + r];  // Mt[c=r][r'=q] = X[q][r]
+    Li[(size_t)q * ld + r] = T[r * CS + q];  // Linv[r][q]    = X[r][q]
+  }
+}
+__global__ __launch_bounds__(64) void k_diag_w(DevBatch db, int jt) {
+  __shared__ __attribute__((aligned(16))) double sm[DWS];
+  diag_wave(db, blockIdx.x, jt, sm);
+}
+
 // ============================================================================================
 // Generic batched tile GEMM of the recursion (see GemmOp).  Unit = pair of vertically adjacent
 // 64x64 output tiles in one tile column; wave (wr, wc) = tile wr of the pair, columns 32wc..+31.
@@ -929,7 +1071,8 @@ void launch_gram(const DevBatch& b, hipStream_t s) {
   hipLaunchKernelGGL(k_gram, dim3(grid_blocks(b.B, b.ntl)), dim3(NTHR), gram_lds(b.d), s, b);
 }
 void launch_diag(const DevBatch& b, int jt, hipStream_t s) {
-  hipLaunchKernelGGL(k_diag, dim3(b.B), dim3(NTHR), 0, s, b, jt);
+  if (b.diag_variant == 1) hipLaunchKernelGGL(k_diag_w, dim3(b.B), dim3(64), 0, s, b, jt);
+  else hipLaunchKernelGGL(k_diag, dim3(b.B), dim3(NTHR), 0, s, b, jt);
 }
 void launch_leaf(const DevBatch& b, int o, int n, hipStream_t s) {
   hipLaunchKernelGGL(k_leaf, dim3(b.B), dim3(NTHR), 0, s, b, o, n);
@@ -944,7 +1087,8 @@ void launch_gemm(const DevBatch& b, const GemmGeom& g, hipStream_t s, const Gemm
     T += pair_units(R, C, tri);
   }
   const dim3 grid(grid_blocks(b.B, T));
-  switch (b.gemm_variant) {
+  const int variant = (g.op != OP_PREDVAR && g.n <= b.small_n) ? b.gemm_variant_small : b.gemm_variant;
+  switch (variant) {
     case 1: hipLaunchKernelGGL(k_gemm_w3, grid, dim3(NTHR), 0, s, b, g, g2); break;
     case 2: hipLaunchKernelGGL(k_gemm_s1, grid, dim3(NTHR), 0, s, b, g, g2); break;
     default: hipLaunchKernelGGL(k_gemm, grid, dim3(NTHR), 0, s, b, g, g2); break;

@@ -32,15 +32,20 @@ class BackTracking:
 
     def __call__(self, phi, alpha_0: float, phi_0: float, dphi_0: float):
         """LineSearches.BackTracking: returns (alpha, phi(alpha)); raises LineSearchError."""
+        return _drive(self.search(alpha_0, phi_0, dphi_0), phi)
+
+    def search(self, alpha_0: float, phi_0: float, dphi_0: float):
+        """The same search as a generator: yields each step length to evaluate, receives phi(a),
+        returns (alpha, phi(alpha)) -- so a batch of independent searches can share device calls."""
         iterfinitemax = -math.log2(np.finfo(float).eps)
         a1 = a2 = alpha_0
-        phix0, phix1 = phi_0, phi(a1)
+        phix0, phix1 = phi_0, (yield a1)
         it_fin = 0
         while not math.isfinite(phix1) and it_fin < iterfinitemax:
             it_fin += 1
             a1 = a2
             a2 = a1 / 2
-            phix1 = phi(a2)
+            phix1 = yield a2
         it = 0
         while phix1 > phix0 + self.c_1 * a2 * dphi_0:
             it += 1
@@ -60,8 +65,18 @@ class BackTracking:
             atmp = _nanmin(atmp, a2 * self.rho_hi)
             a1 = a2
             a2 = _nanmax(atmp, a2 * self.rho_lo)
-            phix0, phix1 = phix1, phi(a2)
+            phix0, phix1 = phix1, (yield a2)
         return a2, phix1
+
+
+def _drive(gen, fn):
+    """Run a request generator to completion, answering each yielded request with fn(request)."""
+    try:
+        req = next(gen)
+        while True:
+            req = gen.send(fn(req))
+    except StopIteration as e:
+        return e.value
 
 
 class LineSearchError(Exception):
@@ -138,23 +153,26 @@ def lbfgs_minimize(f, fg, x0, method: LBFGS | None = None, options: Options | No
     """Optim.optimize(OnceDifferentiable(f, g!, fg!), x0, LBFGS(...), options).
 
     f(x) -> value; fg(x) -> (value, gradient).  Values may be +inf (failed evaluations)."""
+
+    def answer(req):
+        kind, x = req
+        return f(x) if kind == "f" else fg(x)
+
+    return _drive(lbfgs_steps(x0, method, options), answer)
+
+
+def lbfgs_steps(x0, method: LBFGS | None = None, options: Options | None = None):
+    """LBFGS as a request generator: yields ("f", x) or ("fg", x), receives f(x) or (f(x), g(x)),
+    returns the Result.  lbfgs_minimize drives one; optimize_batch drives a batch in lock-step."""
     method = method or LBFGS()
     options = options or Options()
     t0 = time.time()
     calls = {"f": 0, "g": 0}
 
-    def count(kind):
+    def budget(kind):
         calls[kind] += 1
         if options.max_evals is not None and calls["f"] + calls["g"] > options.max_evals:
             raise _Budget()
-
-    def F(x):
-        count("f")
-        return f(x)
-
-    def FG(x):
-        count("g")
-        return fg(x)
 
     x = np.array(x0, dtype=np.float64)
     n = x.shape[0]
@@ -164,8 +182,11 @@ def lbfgs_minimize(f, fg, x0, method: LBFGS | None = None, options: Options | No
     rho = np.zeros(m)
     stopped = "iterations"
     it = 0
+    fx = math.nan
+    converged = False
     try:
-        fx, g = FG(x)
+        budget("g")
+        fx, g = yield ("fg", x)
         pseudo = 0
         converged = bool(np.max(np.abs(g)) <= options.g_abstol)
         while not converged and it < options.iterations:
@@ -178,15 +199,20 @@ def lbfgs_minimize(f, fg, x0, method: LBFGS | None = None, options: Options | No
                 pseudo = 1
                 s = -g
                 dphi0 = float(g @ s)
-            phi = lambda a: F(x + a * s)
+            ls = method.linesearch.search(method.alphaguess, fx, dphi0)
             try:
-                alpha, _ = method.linesearch(phi, method.alphaguess, fx, dphi0)
-                ls_ok = True
+                a = next(ls)
+                while True:
+                    budget("f")
+                    a = ls.send((yield ("f", x + a * s)))
+            except StopIteration as e:
+                alpha, ls_ok = e.value[0], True
             except LineSearchError as e:
                 alpha, ls_ok = e.alpha, False
             dx = alpha * s
             x = x + dx
-            fx, g = FG(x)
+            budget("g")
+            fx, g = yield ("fg", x)
             dg = g - g_prev
             denom = float(dx @ dg)
             r = 1.0 / denom if denom != 0 else math.inf
@@ -237,3 +263,55 @@ def optimize(gp, method: LBFGS | None = None, options: Options | None = None) ->
         gp.update_mll()
         raise
     return res
+
+
+def optimize_batch(batch, theta0, method: LBFGS | None = None, options: Options | None = None):
+    """One LBFGS run per slot of a GPBatch (the per-output GPs of CPnoise.jl:37-43 and the trials
+    of examples/parallel/core.jl:28), in lock-step: every round answers all pending requests with
+    ONE device evaluation of the whole batch (value + gradient for every slot).  Each slot follows
+    exactly the trajectory lbfgs_minimize would give it alone (the requests and their answers are
+    the same; only the device calls are shared).  A gradient computed during the line search is
+    reused when that point is accepted.  Failed slots answer +Inf as in `optimize`.
+    Returns (results, rounds)."""
+    theta0 = np.asarray(theta0, dtype=np.float64)
+    B, npar = theta0.shape
+    gens = [lbfgs_steps(theta0[s], method, options) for s in range(B)]
+    results = [None] * B
+    pending = [None] * B
+    for s in range(B):
+        try:
+            pending[s] = next(gens[s])
+        except StopIteration as e:
+            results[s] = e.value
+    cache = [None] * B  # (x, f, g) of the slot's last evaluation
+    rounds = 0
+    while any(p is not None for p in pending):
+        todo = []
+        th = theta0.copy()
+        for s, req in enumerate(pending):
+            if req is None:
+                continue
+            x = req[1]
+            if cache[s] is not None and np.array_equal(cache[s][0], x):
+                continue
+            todo.append(s)
+            th[s] = x if np.all(np.isfinite(x)) else theta0[s]
+        if todo:
+            rounds += 1
+            r = batch.run(th, grad=True, predict=False)
+            for s in todo:
+                x = pending[s][1]
+                if r["status"][s] != 0 or not np.all(np.isfinite(x)):
+                    cache[s] = (x.copy(), math.inf, np.full(npar, math.nan))
+                else:
+                    cache[s] = (x.copy(), -float(r["mll"][s]), -np.asarray(r["grad"][s], dtype=np.float64))
+        for s, req in enumerate(pending):
+            if req is None:
+                continue
+            _, f, g = cache[s]
+            try:
+                pending[s] = gens[s].send(f if req[0] == "f" else (f, g.copy()))
+            except StopIteration as e:
+                pending[s] = None
+                results[s] = e.value
+    return results, rounds

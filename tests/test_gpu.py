@@ -192,3 +192,47 @@ def test_gpu_evaluator_for_sharding(gprx, ctx, golden_dir):
     G = z["Y"].shape[0]
     r = ev(z["X"], z["Y"], np.tile(z["theta"], (G, 1)), z["Xs"])
     np.testing.assert_allclose(r["mll"], z["mll_exp"], rtol=TOL_MLL)
+
+
+def test_optimize_batch_matches_single_gp_runs(gprx, ctx, golden_dir):
+    """Lock-step batched LBFGS (one device call per round for all slots) gives every slot the
+    same trajectory as optimising its GP alone through the GPE mirror (CPnoise.jl:37-43 loop)."""
+    from gprx.optim import LBFGS, Options, optimize, optimize_batch
+
+    z = np.load(golden_dir / "cp_n64.npz")
+    X, Y, th = z["X"], z["Y"], z["theta"]
+    B = Y.shape[0]
+    opts = Options(max_evals=20)
+    b = gprx.GPBatch(B, X.shape[0], X.shape[1], 0, ctx=ctx)
+    b.set_train(X, Y)
+    res, rounds = optimize_batch(b, np.tile(th, (B, 1)), LBFGS(), opts)
+    assert rounds < sum(r.f_calls + r.g_calls for r in res)
+    for s in range(B):
+        gp = gprx.GP(X, Y[s], gprx.MeanZero(), gprx.SEArd(th[1:-1], th[-1]), ctx=ctx)
+        ref = optimize(gp, LBFGS(), opts)
+        np.testing.assert_array_equal(res[s].minimizer, ref.minimizer)
+        assert res[s].minimum == ref.minimum
+
+
+def test_graph_replay_matches_direct_launches(gprx, golden_dir, monkeypatch):
+    """The hipGraph replay (default) and direct stream launches give bit-identical results,
+    including after the test set (and so the captured geometry) changes."""
+    z = np.load(golden_dir / "p2_n256.npz")
+    X, Y, th, Xs = z["X"], z["Y"], z["theta"], z["Xs"]
+    out = []
+    for graphs in ("1", "0"):
+        monkeypatch.setenv("GPRX_GRAPHS", graphs)
+        c = gprx.Context(0)
+        b = gprx.GPBatch(Y.shape[0], X.shape[0], X.shape[1], Xs.shape[1], ctx=c)
+        b.set_train(X, Y)
+        b.set_test(Xs)
+        r1 = b.run(np.tile(th, (Y.shape[0], 1)), grad=True, predict=True)
+        b.set_test(Xs[:, :7])
+        r2 = b.run(np.tile(th, (Y.shape[0], 1)), grad=True, predict=True)
+        out.append((r1, r2))
+        b.close()
+        c.close()
+    for k in ("mll", "grad", "mu", "var"):
+        np.testing.assert_array_equal(out[0][0][k], out[1][0][k])
+        np.testing.assert_array_equal(out[0][1][k], out[1][1][k])
+    np.testing.assert_array_equal(out[0][1]["mu"], out[0][0]["mu"][:, :7])

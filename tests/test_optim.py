@@ -70,3 +70,58 @@ def test_lbfgs_improves_gp_target(golden_dir):
 
     r = lbfgs_minimize(f, fg, th0, LBFGS(), Options(max_evals=40))
     assert r.minimum < f(th0)
+
+
+class _OracleBatch:
+    """Stand-in for GPBatch.run backed by the oracle (CPU): same per-slot contract."""
+
+    def __init__(self, X, Ys):
+        self.X, self.Ys = X, Ys
+        self.calls = 0
+
+    def run(self, theta, grad=True, predict=False):
+        self.calls += 1
+        B = theta.shape[0]
+        mll = np.empty(B)
+        g = np.empty_like(theta)
+        st = np.zeros(B, dtype=np.int32)
+        for s in range(B):
+            try:
+                m, gg, _ = O.lml(self.X, self.Ys[s], theta[s], want_grad=True)
+                mll[s], g[s] = m, gg
+            except O.NotPosDef:
+                st[s] = 1
+        return dict(mll=mll, grad=g, status=st)
+
+
+def test_optimize_batch_matches_sequential(golden_dir):
+    from gprx.optim import optimize_batch
+
+    z = np.load(golden_dir / "p1_n50.npz")
+    X, Ys, th0 = z["X"], z["Y"], z["theta"]
+    B = Ys.shape[0]
+    rng = np.random.default_rng(4)
+    thetas = np.stack([th0 + 0.1 * rng.standard_normal(th0.shape[0]) for _ in range(B)])
+    opts = Options(max_evals=25)
+    fake = _OracleBatch(X, Ys)
+    res, rounds = optimize_batch(fake, thetas, LBFGS(), opts)
+    for s in range(B):
+
+        def f(h, s=s):
+            try:
+                return -O.lml(X, Ys[s], h)[0]
+            except O.NotPosDef:
+                return math.inf
+
+        def fg(h, s=s):
+            try:
+                m, g, _ = O.lml(X, Ys[s], h, want_grad=True)
+                return -m, -g
+            except O.NotPosDef:
+                return math.inf, np.full(h.shape[0], np.nan)
+
+        ref = lbfgs_minimize(f, fg, thetas[s], LBFGS(), opts)
+        np.testing.assert_array_equal(res[s].minimizer, ref.minimizer)
+        assert res[s].minimum == ref.minimum and res[s].stopped_by == ref.stopped_by
+    # lock-step sharing: far fewer batch calls than the total number of evaluations
+    assert rounds == fake.calls and rounds <= max(r.f_calls + r.g_calls for r in res)
