@@ -42,7 +42,9 @@ struct gprx_ctx {
   std::vector<hipEvent_t> evpool;
   std::vector<PendingEv> pending;
   int nstreams = 1;                   // slot groups run concurrently on these streams (1: measured best)
-  int leaf_tiles = 4;                 // recursion nodes of <= this many tiles run fused (k_leaf)
+  // recursion nodes of <= this many tiles run fused in k_leaf; 0 = auto: 4 for batches of >= 32
+  // slots (fewer launches), 1 below that (the one-wave diag chain has the lowest latency)
+  int leaf_tiles = 0;
   bool fuse_tt = true;                // TT shares the SYRK launch (env GPRX_FUSE_TT=0 to split)
   // replay each batch's launch sequence as a hipGraph (GPRX_GRAPHS=1).  Off by default: measured
   // equal to direct launches at B=1..192 (the launches are queued far ahead of the GPU).
@@ -236,7 +238,8 @@ int copy_in(gprx_ctx* c, void* dst, const void* src, size_t bytes, int mem) {
 // Recursive Cholesky + inverse over tile range [o, o+n) (tile units), all slots in lock step.
 void factor_rec(gprx_ctx* c, hipStream_t st, const DevBatch& db, int o, int n) {
   const double T = TS, Bd = db.B;
-  if (n > 1 && n <= c->leaf_tiles) {
+  const int leaf = c->leaf_tiles > 0 ? c->leaf_tiles : (db.B >= 32 ? 4 : 1);
+  if (n > 1 && n <= leaf) {
     const double m = n * T;
     timed(c, st, "leaf", Bd * (m * m * m / 3.0 + m * m * m / 3.0), Bd * 8.0 * 3.0 * m * m,
           [&] { gprx::launch_leaf(db, o, n, st); }, n);
@@ -384,7 +387,7 @@ int gprx_ctx_create(int device, gprx_ctx** out) {
   if (const char* ns = getenv("GPRX_STREAMS")) c->nstreams = atoi(ns) > 0 ? atoi(ns) : 1;
   if (const char* ft = getenv("GPRX_FUSE_TT")) c->fuse_tt = atoi(ft) != 0;
   if (const char* gr = getenv("GPRX_GRAPHS")) c->use_graphs = atoi(gr) != 0;
-  if (const char* lt = getenv("GPRX_LEAF")) c->leaf_tiles = atoi(lt) >= 1 && atoi(lt) <= 8 ? atoi(lt) : 4;
+  if (const char* lt = getenv("GPRX_LEAF")) c->leaf_tiles = atoi(lt) >= 0 && atoi(lt) <= 8 ? atoi(lt) : 0;
   c->gstreams.resize(c->nstreams);
   c->gevents.resize(1 + c->nstreams);
   for (auto& st : c->gstreams)

@@ -30,11 +30,18 @@ __device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
-// blockIdx -> (slot, unit).  Slot s runs on the blocks b with b % 8 == s % 8, i.e. on one XCD
-// under the dispatcher's round-robin placement (speed only, never correctness).  The grid is
-// padded to 8 * ceil(B/8) * T blocks; surplus blocks return at once.
-__host__ __device__ inline int grid_blocks(int B, int T) { return 8 * ((B + 7) / 8) * T; }
+// blockIdx -> (slot, unit).  With B >= 8, slot s runs on the blocks b with b % 8 == s % 8, i.e.
+// on one XCD under the dispatcher's round-robin placement (speed only, never correctness), so
+// its panels stay in one L2; the grid is padded to 8 * ceil(B/8) * T blocks and surplus blocks
+// return at once.  With B < 8 that would leave XCDs idle, so a slot's units are spread over
+// all of them (linear mapping).
+__host__ __device__ inline int grid_blocks(int B, int T) { return B < 8 ? B * T : 8 * ((B + 7) / 8) * T; }
 __device__ __forceinline__ bool map_block(int bid, int B, int T, int& slot, int& unit) {
+  if (B < 8) {
+    slot = bid / T;
+    unit = bid - slot * T;
+    return slot < B;
+  }
   const int x = bid & 7, q = bid >> 3;
   slot = (q / T) * 8 + x;
   unit = q % T;
