@@ -790,13 +790,13 @@ __global__ __launch_bounds__(NTHR) void k_alpha(DevBatch db, int phase) {
 // ============================================================================================
 template <int V>
 __device__ __forceinline__ void lauum_body(const DevBatch& db) {
+  // LDS: x of the unit's three tiles, [p][64] each (3*d*64 doubles, 39 KB at d = 26, so four
+  // workgroups fit a CU); the per-wave partial sums reuse it after the last x read.
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int d = db.d, tid = threadIdx.x, w = tid >> 6, wr = w >> 1, wc = w & 1;
   double* xr_s = sm;                // [2][d][64] rows of ti, ti+1
   double* xc_s = sm + 2 * d * TS;   // [d][64]    rows of tj
-  double* al_s = sm + 3 * d * TS;   // [3][64]
-  double* pw = al_s + 3 * TS;       // [d+3]
-  double* sp = pw + DMAX + 4;       // [4][d+2]
+  double* sp = sm;                  // [4][d+2] after phase 2
   const int nt = db.nt;
   int slot, u, pr, tj;
   if (!map_block(blockIdx.x, db.B, pair_units(nt, nt, true), slot, u)) return;
@@ -810,13 +810,6 @@ __device__ __forceinline__ void lauum_body(const DevBatch& db) {
     xr_s[d * TS + p * TS + r] = (pr + 1 < nt) ? X[(size_t)(pr + 1) * TS * d + e] : 0.0;
     xc_s[p * TS + r] = X[(size_t)tj * TS * d + e];
   }
-  if (tid < TS) {
-    al_s[tid] = al[pr * TS + tid];
-    al_s[TS + tid] = (pr + 1 < nt) ? al[(pr + 1) * TS + tid] : 0.0;
-    al_s[2 * TS + tid] = al[tj * TS + tid];
-  }
-  const double* P = db.params + (size_t)slot * db.pst;
-  for (int e = tid; e < d + 3; e += NTHR) pw[e] = P[e];
   const int ti = pr + wr;
   const bool active = ti < nt;
   const int l = tid & 63, lr = l & 15, lk = l >> 4, mode = db.dist_mode;
@@ -831,6 +824,13 @@ __device__ __forceinline__ void lauum_body(const DevBatch& db) {
   const double* xr = xr_s + wr * d * TS;
   const double* KF = db.KF + so + (size_t)(tj * TS + 32 * wc) * ld + ti * TS;
   if (active) {
+    double ar[WM], ac[WN][4];
+#pragma unroll
+    for (int a = 0; a < WM; ++a) ar[a] = al[ti * TS + 16 * a + lr];
+#pragma unroll
+    for (int b = 0; b < WN; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) ac[b][q] = al[tj * TS + 32 * wc + 16 * b + lk + 4 * q];
     // G in place of acc
 #pragma unroll
     for (int a = 0; a < WM; ++a)
@@ -843,7 +843,7 @@ __device__ __forceinline__ void lauum_body(const DevBatch& db) {
           double G = 0.0;
           if (gi < db.N && gj < db.N && gi >= gj) {
             const double kf = KF[(size_t)(16 * b + lk + 4 * q) * ld + r];
-            const double W = al_s[wr * TS + r] * al_s[2 * TS + c] - acc[a][b][q];
+            const double W = ar[a] * ac[b][q] - acc[a][b][q];
             if (gi == gj) {
               G = 0.5 * (W * kf);
               tr += W;
@@ -856,6 +856,7 @@ __device__ __forceinline__ void lauum_body(const DevBatch& db) {
         }
   }
   // S_p, one dimension at a time; x values of this lane's 4 rows / 8 columns from LDS
+  double spv = 0.0;  // lane p < d keeps S_p of this wave
   for (int p = 0; p < d; ++p) {
     double s = 0.0;
     if (active && !(db.ablate & 2)) {
@@ -880,24 +881,26 @@ __device__ __forceinline__ void lauum_body(const DevBatch& db) {
           for (int q = 0; q < 4; ++q) s = fma(acc[a][b][q], sqd2(xa[a], xa2[a], xb[b][q], xb2[b][q], mode), s);
     }
     s = wave_sum(s);
-    if (l == 0) sp[w * (DMAX + 2) + p] = s;
+    spv = (l == p) ? s : spv;
   }
   sf = wave_sum(sf);
   tr = wave_sum(tr);
-  if (l == 0) {
-    sp[w * (DMAX + 2) + d] = sf;
-    sp[w * (DMAX + 2) + d + 1] = tr;
-  }
+  spv = (l == d) ? sf : (l == d + 1 ? tr : spv);
+  __syncthreads();  // every wave is done with the x tiles: reuse them for the partials
+  if (l < d + 2) sp[w * (d + 2) + l] = spv;
   __syncthreads();
   double* out = db.grad_part + ((size_t)slot * db.ngu + u) * db.gps;
   for (int e = tid; e < d + 2; e += NTHR)
-    out[e] = ((sp[e] + sp[(DMAX + 2) + e]) + sp[2 * (DMAX + 2) + e]) + sp[3 * (DMAX + 2) + e];
+    out[e] = ((sp[e] + sp[(d + 2) + e]) + sp[2 * (d + 2) + e]) + sp[3 * (d + 2) + e];
 }
 __global__ __launch_bounds__(NTHR) void k_lauum_grad(DevBatch db) { lauum_body<0>(db); }
 __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_lauum_grad_w3(DevBatch db) {
   lauum_body<0>(db);
 }
 __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_lauum_grad_s1(DevBatch db) {
+  lauum_body<2>(db);
+}
+__global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_lauum_grad_o4(DevBatch db) {
   lauum_body<2>(db);
 }
 int lauum_units(int nt) { return pair_units(nt, nt, true); }
@@ -1060,7 +1063,10 @@ __global__ __launch_bounds__(NTHR) void k_pred_final(DevBatch db) {
 // launchers
 // ---------------------------------------------------------------------------------------------
 static size_t gram_lds(int d) { return (size_t)(2 * d * TS + DMAX + 4) * sizeof(double); }
-static size_t lauum_lds(int d) { return (size_t)(3 * d * TS + 3 * TS + DMAX + 4 + 4 * (DMAX + 2)) * sizeof(double); }
+static size_t lauum_lds(int d) {
+  const int xs = 3 * d * TS, ps = 4 * (d + 2);
+  return (size_t)(xs > ps ? xs : ps) * sizeof(double);
+}
 static size_t cross_lds(int d) { return (size_t)(2 * d * TS + DMAX + 4 + TS + 16 * TS) * sizeof(double); }
 
 static void set_lds_limits() {
@@ -1068,7 +1074,8 @@ static void set_lds_limits() {
   if (done) return;
   done = true;
   (void)hipFuncSetAttribute((const void*)k_gram, hipFuncAttributeMaxDynamicSharedMemorySize, (int)gram_lds(DMAX));
-  for (const void* f : {(const void*)k_lauum_grad, (const void*)k_lauum_grad_w3, (const void*)k_lauum_grad_s1})
+  for (const void* f : {(const void*)k_lauum_grad, (const void*)k_lauum_grad_w3, (const void*)k_lauum_grad_s1,
+                        (const void*)k_lauum_grad_o4})
     (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lauum_lds(DMAX));
   (void)hipFuncSetAttribute((const void*)k_pred_cross, hipFuncAttributeMaxDynamicSharedMemorySize, (int)cross_lds(DMAX));
 }
@@ -1110,6 +1117,7 @@ void launch_lauum_grad(const DevBatch& b, hipStream_t s) {
   switch (b.lauum_variant) {
     case 1: hipLaunchKernelGGL(k_lauum_grad_w3, grid, dim3(NTHR), lauum_lds(b.d), s, b); break;
     case 2: hipLaunchKernelGGL(k_lauum_grad_s1, grid, dim3(NTHR), lauum_lds(b.d), s, b); break;
+    case 3: hipLaunchKernelGGL(k_lauum_grad_o4, grid, dim3(NTHR), lauum_lds(b.d), s, b); break;
     default: hipLaunchKernelGGL(k_lauum_grad, grid, dim3(NTHR), lauum_lds(b.d), s, b); break;
   }
 }

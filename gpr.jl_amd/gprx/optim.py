@@ -52,16 +52,16 @@ class BackTracking:
             if it > self.iterations:
                 raise LineSearchError(a2)
             if self.order == 2 or it == 1:
-                atmp = -(dphi_0 * a2 * a2) / (2 * (phix1 - phix0 - dphi_0 * a2))
+                atmp = _div(-(dphi_0 * a2 * a2), 2 * (phix1 - phix0 - dphi_0 * a2))
             else:
-                div = 1.0 / (a1 * a1 * a2 * a2 * (a2 - a1))
+                div = _div(1.0, a1 * a1 * a2 * a2 * (a2 - a1))
                 a = (a1 * a1 * (phix1 - phi_0 - dphi_0 * a2) - a2 * a2 * (phix0 - phi_0 - dphi_0 * a1)) * div
                 b = (-a1**3 * (phix1 - phi_0 - dphi_0 * a2) + a2**3 * (phix0 - phi_0 - dphi_0 * a1)) * div
                 if abs(a) <= np.finfo(float).eps:
-                    atmp = dphi_0 / (2 * b)
+                    atmp = _div(dphi_0, 2 * b)
                 else:
                     disc = max(b * b - 3 * a * dphi_0, 0.0)
-                    atmp = (-b + math.sqrt(disc)) / (3 * a)
+                    atmp = _div(-b + math.sqrt(disc), 3 * a)
             atmp = _nanmin(atmp, a2 * self.rho_hi)
             a1 = a2
             a2 = _nanmax(atmp, a2 * self.rho_lo)
@@ -83,6 +83,12 @@ class LineSearchError(Exception):
     def __init__(self, alpha):
         super().__init__("line search failed to converge")
         self.alpha = alpha
+
+
+def _div(a, b) -> float:
+    """a / b with IEEE (Julia) semantics: x/0 -> +-Inf, 0/0 -> NaN, never an exception."""
+    with np.errstate(divide="ignore", invalid="ignore"):
+        return float(np.float64(a) / np.float64(b))
 
 
 def _nanmin(a, b):
@@ -137,7 +143,8 @@ def _twoloop(g, rho, dxh, dgh, m, pseudo_it, scaleinvH0):
         q -= alpha[i] * dgh[i]
     if scaleinvH0 and pseudo_it > 1:
         i = (upper - 1) % m
-        s = (float(dxh[i] @ dgh[i]) / float(dgh[i] @ dgh[i])) * q
+        with np.errstate(divide="ignore", invalid="ignore"):  # Julia float semantics: x/0 -> Inf/NaN
+            s = (np.float64(dxh[i] @ dgh[i]) / np.float64(dgh[i] @ dgh[i])) * q
     else:
         s = q.copy()
     for index in range(lower, upper + 1):
@@ -215,7 +222,7 @@ def lbfgs_steps(x0, method: LBFGS | None = None, options: Options | None = None)
             fx, g = yield ("fg", x)
             dg = g - g_prev
             denom = float(dx @ dg)
-            r = 1.0 / denom if denom != 0 else math.inf
+            r = _div(1.0, denom)
             if not math.isinf(r):
                 i = (pseudo - 1) % m
                 dxh[i] = dx.copy()

@@ -43,9 +43,10 @@ def kernel_params(theta: np.ndarray, d: int):
     """
     theta = np.asarray(theta, dtype=np.float64)
     assert theta.shape == (d + 2,)
-    il2 = np.exp(-2.0 * theta[1 : d + 1])
-    sf2 = math.exp(2.0 * theta[d + 1])
-    sn2 = math.exp(2.0 * theta[0])
+    with np.errstate(over="ignore"):  # Julia exp overflows to Inf (then cholesky fails)
+        il2 = np.exp(-2.0 * theta[1 : d + 1])
+        sf2 = float(np.exp(2.0 * theta[d + 1]))
+        sn2 = float(np.exp(2.0 * theta[0]))
     return il2, sf2, sn2, sn2 + EPS
 
 
@@ -103,6 +104,9 @@ def cholesky_upper(K: np.ndarray) -> np.ndarray:
         raise NotPosDef(int(info))
     if info < 0:
         raise ValueError("dpotrf argument error")
+    dg = np.diag(U)
+    if not np.all(np.isfinite(dg)):  # Inf entries (exp overflow): NaN pivots make dpotrf fail
+        raise NotPosDef(int(np.argmin(np.isfinite(dg))) + 1)
     return U
 
 

@@ -125,3 +125,12 @@ def test_optimize_batch_matches_sequential(golden_dir):
         assert res[s].minimum == ref.minimum and res[s].stopped_by == ref.stopped_by
     # lock-step sharing: far fewer batch calls than the total number of evaluations
     assert rounds == fake.calls and rounds <= max(r.f_calls + r.g_calls for r in res)
+
+
+def test_twoloop_and_linesearch_follow_ieee_division():
+    # a flat objective gives dx . dg = 0 and dg . dg = 0: Julia divides to Inf/NaN, never raises
+    r = lbfgs_minimize(lambda x: 0.0, lambda x: (0.0, np.zeros_like(x)), np.ones(3))
+    assert r.converged
+    f = lambda x: float(abs(x[0]))  # kink: identical gradients on one side
+    r = lbfgs_minimize(f, lambda x: (f(x), np.array([np.sign(x[0])])), np.array([3.0]), options=Options(max_evals=20))
+    assert r.f_calls + r.g_calls <= 21
