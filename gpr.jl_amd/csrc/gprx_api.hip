@@ -123,6 +123,7 @@ DevBatch sub_batch(const DevBatch& db, int s0, int cnt) {
   const size_t s = s0;
   v.B = cnt;
   v.X += s * db.Npad * db.d;
+  v.Xc += s * db.Npad * db.xs;
   v.Y += s * db.Npad;
   v.K += s * db.mat;
   v.KF += s * db.mat;
@@ -482,6 +483,8 @@ int gprx_batch_create(gprx_ctx* c, int B, int d, int N, int M_max, gprx_batch** 
     return r;
   };
   if ((rc = dalloc(b, &db.X, Bs * db.Npad * d))) return fail(rc);
+  db.xs = 16 * ((d + 15) / 16) + 2;
+  if ((rc = dalloc(b, &db.Xc, Bs * db.Npad * db.xs))) return fail(rc);
   if ((rc = dalloc(b, &db.Y, Bs * db.Npad))) return fail(rc);
   if ((rc = dalloc(b, &db.K, Bs * db.mat))) return fail(rc);
   if ((rc = dalloc(b, &db.KF, Bs * db.mat))) return fail(rc);
@@ -556,6 +559,8 @@ int gprx_batch_set_train(gprx_batch* b, const double* X, int64_t xs, const doubl
       return rc;
     if ((rc = copy_in(c, db.Y + (size_t)s * db.Npad, Y + (size_t)s * ys, (size_t)db.N * sizeof(double), mem))) return rc;
   }
+  gprx::launch_center(db, c->stream);
+  HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipStreamSynchronize(c->stream));
   b->have_train = true;
   b->factored = false;

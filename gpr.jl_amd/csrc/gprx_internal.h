@@ -29,11 +29,15 @@ struct DevBatch {
   int small_n;                 // (GPRX_SMALL_N)
   int lauum_variant;           // k_lauum_grad variant (env GPRX_LAUUMV; experiments)
   int diag_variant;            // 0: 4-wave k_diag, 1: one-wave k_diag_w (env GPRX_DIAGV)
+  int xs;                      // row stride of Xc: 16 ceil(d/16) + 2 (conflict-free LDS row reads)
   int pst;                     // stride of params per slot
   int gps;                     // stride of per-unit gradient partials (d + 2)
   int ngu;                     // gradient partial units per slot
   size_t ld, mat;              // ld = Npad, mat = Npad*Npad
   double* X;                   // B x [Npad][d]   (column t = one CState, contiguous d values)
+  double* Xc;                  // B x [Npad][xs]  X minus its per-dimension mean over the N points,
+                               //                 dimensions d..xs-1 zero (theta-independent; the
+                               //                 gradient's distance sums)
   double* Y;                   // B x Npad        (y - mean(X), zero padded)
   double* K;                   // B x mat
   double* KF;                  // B x mat
@@ -87,6 +91,7 @@ __host__ __device__ inline void op_rect(const GemmGeom& g, int nt, int mt, int& 
 
 // kernel launchers (gprx_kernels.hip); every launcher is asynchronous on `s`
 void launch_gram(const DevBatch& b, hipStream_t s);
+void launch_center(const DevBatch& b, hipStream_t s);
 void launch_diag(const DevBatch& b, int jt, hipStream_t s);
 void launch_leaf(const DevBatch& b, int o, int n, hipStream_t s);
 // one launch; with g2.op != OP_NONE the units of g2 are appended to g's (independent ops)

@@ -275,15 +275,13 @@ __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
   }
 }
 
-// Centred copy of the training points: Xc[t][p] = X[t][p] - mean_t X[t][p] for t < N, p < d, and 0
-// elsewhere (padded points, padded dimensions up to the stride xs).  grid = B, once per
-// gprx_batch_set_train.
+// Centred copy of the training points: Xc = X - mean over the N points, per dimension (padded
+// points 0).  grid = B, once per gprx_batch_set_train.
 __global__ __launch_bounds__(NTHR) void k_center(DevBatch db) {
-  __shared__ double mean[DMAX];
   __shared__ double red[4];
-  const int slot = blockIdx.x, tid = threadIdx.x, d = db.d, xs = db.xs;
+  const int slot = blockIdx.x, tid = threadIdx.x, d = db.d;
   const double* X = db.X + (size_t)slot * db.Npad * d;
-  double* Xc = db.Xc + (size_t)slot * db.Npad * xs;
+  double* Xc = db.Xc + (size_t)slot * db.Npad * d;
   for (int p = 0; p < d; ++p) {
     double s = 0.0;
     for (int t = tid; t < db.N; t += NTHR) s += X[(size_t)t * d + p];
@@ -291,12 +289,8 @@ __global__ __launch_bounds__(NTHR) void k_center(DevBatch db) {
     __syncthreads();
     if ((tid & 63) == 0) red[tid >> 6] = s;
     __syncthreads();
-    if (tid == 0) mean[p] = (((red[0] + red[1]) + red[2]) + red[3]) / db.N;
-  }
-  __syncthreads();
-  for (int e = tid; e < db.Npad * xs; e += NTHR) {
-    const int t = e / xs, p = e - t * xs;
-    Xc[e] = (t < db.N && p < d) ? X[(size_t)t * d + p] - mean[p] : 0.0;
+    const double mean = (((red[0] + red[1]) + red[2]) + red[3]) / db.N;
+    for (int t = tid; t < db.Npad; t += NTHR) Xc[(size_t)t * d + p] = t < db.N ? X[(size_t)t * d + p] - mean : 0.0;
   }
 }
 
@@ -838,16 +832,16 @@ template <int V>
 __device__ __forceinline__ void lauum_body(const DevBatch& db) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int d = db.d, tid = threadIdx.x, w = tid >> 6, wr = w >> 1, wc = w & 1;
-  const int xs = db.xs, xt = TS * xs;  // point-tile image: [64][xs], dims >= d zero
-  double* xr_s = sm;                    // [2][64][xs] rows of ti, ti+1
-  double* xc_s = sm + 2 * xt;           // [64][xs]    rows of tj
+  const int xt = TS * d;           // doubles per point tile
+  double* xr_s = sm;               // [2][64][d] rows of ti, ti+1
+  double* xc_s = sm + 2 * xt;      // [64][d]    rows of tj
   double* sp = sm + 3 * xt;        // [4][SPW]
   const int nt = db.nt;
   int slot, u, pr, tj;
   if (!map_block(blockIdx.x, db.B, pair_units(nt, nt, true), slot, u)) return;
   pr = db.lauum_order[2 * u];  // units sorted by first row (longest K range first)
   tj = db.lauum_order[2 * u + 1];
-  const double* X = db.Xc + (size_t)slot * db.Npad * xs;
+  const double* X = db.Xc + (size_t)slot * db.Npad * d;
   const double* al = db.alpha + (size_t)slot * db.Npad;
   dma_tile(xr_s, X + (size_t)pr * xt, xt);
   if (pr + 1 < nt) dma_tile(xr_s + xt, X + (size_t)(pr + 1) * xt, xt);
@@ -867,7 +861,7 @@ __device__ __forceinline__ void lauum_body(const DevBatch& db) {
   double* spw = sp + w * SPW;
   for (int e = l; e < SPW; e += 64) spw[e] = 0.0;
   const double* KF = db.KF + so + (size_t)(tj * TS + 32 * wc) * ld + ti * TS;
-  if (active && !(db.ablate & 2)) {
+  if (active) {
     double ar[WM], ac[WN][4];
 #pragma unroll
     for (int a = 0; a < WM; ++a) ar[a] = al[ti * TS + 16 * a + lr];
@@ -923,7 +917,7 @@ __device__ __forceinline__ void lauum_body(const DevBatch& db) {
         s += __shfl_xor(s, 8);
         Cs[b][q] = s;
       }
-    const double* xr = xr_s + wr * xt;  // [r][xs]
+    const double* xr = xr_s + wr * xt;  // [r][d]
     const int H = (d + 15) >> 4;
 #pragma unroll 1
     for (int h = 0; h < H; ++h) {
@@ -936,7 +930,7 @@ __device__ __forceinline__ void lauum_body(const DevBatch& db) {
         for (int b = 0; b < WN; ++b)
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            xa[b][q] = xc_s[(32 * wc + 16 * b + 4 * q + lk) * xs + pA];
+            xa[b][q] = pA < d ? xc_s[(32 * wc + 16 * b + 4 * q + lk) * d + pA] : 0.0;
             t2 = fma(xa[b][q] * xa[b][q], Cs[b][q], t2);
           }
         double t13[4] = {0.0, 0.0, 0.0, 0.0};  // dims p = 16h + lk + 4q'
@@ -946,11 +940,12 @@ __device__ __forceinline__ void lauum_body(const DevBatch& db) {
 #pragma unroll
           for (int b = 0; b < WN; ++b)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) Q = mfma(xa[b][q], acc[a][b][q], Q);
+            for (int q = 0; q < 4; ++q) Q[q] += xa[b][q];
           // lane: row r = 16a + lr; Q[q'] = Q[r][16h + lk + 4q']
 #pragma unroll
           for (int qq = 0; qq < 4; ++qq) {
-            const double x = xr[(16 * a + lr) * xs + 16 * h + lk + 4 * qq];
+            const int p = 16 * h + lk + 4 * qq;
+            const double x = p < d ? xr[(16 * a + lr) * d + p] : 0.0;
             t13[qq] = fma(x, fma(x, R[a], -2.0 * Q[qq]), t13[qq]);
           }
         }
@@ -1159,7 +1154,7 @@ __global__ __launch_bounds__(NTHR) void k_pred_final(DevBatch db) {
 // launchers
 // ---------------------------------------------------------------------------------------------
 static size_t gram_lds(int d) { return (size_t)(2 * d * TS + DMAX + 4) * sizeof(double); }
-static size_t lauum_lds(int d) { return (size_t)(3 * (16 * ((d + 15) / 16) + 2) * TS + 4 * SPW) * sizeof(double); }
+static size_t lauum_lds(int d) { return (size_t)(3 * d * TS + 4 * SPW) * sizeof(double); }
 static size_t cross_lds(int d) { return (size_t)(2 * d * TS + DMAX + 4 + TS + 16 * TS) * sizeof(double); }
 
 static void set_lds_limits() {
