@@ -51,6 +51,9 @@ struct gprx_ctx {
   bool use_graphs = false;
   std::vector<hipStream_t> gstreams;  // group streams
   std::vector<hipEvent_t> gevents;    // fork/join events (1 + nstreams)
+  int stagger = -1;                   // GPRX_STAGGER: -1 groups start together; 0 / 1 group g starts
+                                      // after group g-1's Gram / factorisation
+  std::vector<hipEvent_t> smarks;     // stagger events (nstreams)
 };
 
 struct gprx_batch {
@@ -126,7 +129,6 @@ DevBatch sub_batch(const DevBatch& db, int s0, int cnt) {
   v.Xc += s * db.Npad * db.xs;
   v.Y += s * db.Npad;
   v.K += s * db.mat;
-  v.KF += s * db.mat;
   v.Lw += s * db.mat;
   v.Linv += s * db.mat;
   v.Mt += s * db.mat;
@@ -284,12 +286,16 @@ void predict_group(gprx_ctx* c, hipStream_t st, const DevBatch& db) {
         [&] { gprx::launch_pred_final(db, st); });
 }
 
-// Whole evaluation of one slot group on one stream.
-void eval_group(gprx_ctx* c, hipStream_t st, const DevBatch& db, bool want_grad, bool want_pred) {
+// Whole evaluation of one slot group on one stream.  `mark` (optional) is recorded once the
+// group's factorisation is queued (the stagger point of concurrent slot groups).
+void eval_group(gprx_ctx* c, hipStream_t st, const DevBatch& db, bool want_grad, bool want_pred,
+                hipEvent_t mark = nullptr) {
   const double Bd = db.B, nt = db.nt, Np = db.Npad, d = db.d;
-  timed(c, st, "gram", Bd * 3.0 * db.N * (double)db.N * d / 2.0, Bd * 8.0 * (Np * Np + Np * d),
+  timed(c, st, "gram", Bd * 3.0 * db.N * (double)db.N * d / 2.0, Bd * 8.0 * (Np * Np / 2.0 + Np * d),
         [&] { gprx::launch_gram(db, st); });
+  if (mark && c->stagger == 0) (void)hipEventRecord(mark, st);
   factor_rec(c, st, db, 0, db.nt);
+  if (mark && c->stagger == 1) (void)hipEventRecord(mark, st);
   timed(c, st, "alpha", Bd * Np * Np, Bd * 8.0 * Np * Np / 2.0, [&] { gprx::launch_alpha(db, st, 0); });
   timed(c, st, "alpha", Bd * Np * Np, Bd * 8.0 * Np * Np / 2.0, [&] { gprx::launch_alpha(db, st, 1); });
   if (want_grad)
@@ -344,8 +350,10 @@ int run_groups(gprx_batch* b, bool want_grad, bool want_pred, bool factor) {
     const int cnt = db.B / G + (g < db.B % G ? 1 : 0);
     hipStream_t st = c->gstreams[g];
     HIPCHK(c, hipStreamWaitEvent(st, c->gevents[0], 0));
+    // staggered groups: group g starts when group g-1 has passed its stagger point
+    if (g > 0 && c->stagger >= 0 && factor) HIPCHK(c, hipStreamWaitEvent(st, c->smarks[g - 1], 0));
     const DevBatch v = sub_batch(db, s0, cnt);
-    if (factor) eval_group(c, st, v, want_grad, want_pred);
+    if (factor) eval_group(c, st, v, want_grad, want_pred, c->stagger >= 0 ? c->smarks[g] : nullptr);
     else if (want_pred) predict_group(c, st, v);
     HIPCHK(c, hipEventRecord(c->gevents[1 + g], st));
     HIPCHK(c, hipStreamWaitEvent(c->stream, c->gevents[1 + g], 0));
@@ -389,8 +397,12 @@ int gprx_ctx_create(int device, gprx_ctx** out) {
   if (const char* ft = getenv("GPRX_FUSE_TT")) c->fuse_tt = atoi(ft) != 0;
   if (const char* gr = getenv("GPRX_GRAPHS")) c->use_graphs = atoi(gr) != 0;
   if (const char* lt = getenv("GPRX_LEAF")) c->leaf_tiles = atoi(lt) >= 0 && atoi(lt) <= 8 ? atoi(lt) : 0;
+  if (const char* sg = getenv("GPRX_STAGGER")) c->stagger = atoi(sg);
   c->gstreams.resize(c->nstreams);
   c->gevents.resize(1 + c->nstreams);
+  c->smarks.resize(c->nstreams);
+  for (auto& e : c->smarks)
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return GPRX_DEVICE_ERROR;
   for (auto& st : c->gstreams)
     if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return GPRX_DEVICE_ERROR;
   for (auto& e : c->gevents)
@@ -413,6 +425,7 @@ void gprx_ctx_destroy(gprx_ctx* c) {
     (void)hipStreamDestroy(st);
   }
   for (auto e : c->gevents) (void)hipEventDestroy(e);
+  for (auto e : c->smarks) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -483,11 +496,10 @@ int gprx_batch_create(gprx_ctx* c, int B, int d, int N, int M_max, gprx_batch** 
     return r;
   };
   if ((rc = dalloc(b, &db.X, Bs * db.Npad * d))) return fail(rc);
-  db.xs = 16 * ((d + 15) / 16) + 2;
+  db.xs = 16 * ((d + 15) / 16) + 1;
   if ((rc = dalloc(b, &db.Xc, Bs * db.Npad * db.xs))) return fail(rc);
   if ((rc = dalloc(b, &db.Y, Bs * db.Npad))) return fail(rc);
   if ((rc = dalloc(b, &db.K, Bs * db.mat))) return fail(rc);
-  if ((rc = dalloc(b, &db.KF, Bs * db.mat))) return fail(rc);
   if ((rc = dalloc(b, &db.Lw, Bs * db.mat))) return fail(rc);
   if ((rc = dalloc(b, &db.Linv, Bs * db.mat))) return fail(rc);
   if ((rc = dalloc(b, &db.Mt, Bs * db.mat))) return fail(rc);

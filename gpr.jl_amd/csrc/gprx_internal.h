@@ -14,7 +14,6 @@ constexpr int DMAX = 64;   // largest input dimension d supported (FB: 52)
 // Device-resident state of one batch of B GP slots with equal (d, N).  Passed to every kernel by
 // value.  Matrices are column-major with leading dimension ld = Npad (Npad = ceil(N/64)*64).
 //   K    : Gram matrix (lower tiles), reduced in place by the recursive Cholesky's SYRK updates.
-//   KF   : noise-free Gram matrix Kf (lower tiles), read back by the gradient.
 //   Lw   : recursion workspace: L21 blocks (strictly lower tiles) and T^T = L11^-1 L21^T blocks
 //          (strictly upper tiles).
 //   Linv : L^{-1} (lower).      Mt : L^{-T} (upper) = Linv^T, so that every GEMM streams operands
@@ -29,7 +28,7 @@ struct DevBatch {
   int small_n;                 // (GPRX_SMALL_N)
   int lauum_variant;           // k_lauum_grad variant (env GPRX_LAUUMV; experiments)
   int diag_variant;            // 0: 4-wave k_diag, 1: one-wave k_diag_w (env GPRX_DIAGV)
-  int xs;                      // row stride of Xc: 16 ceil(d/16) + 2 (conflict-free LDS row reads)
+  int xs;                      // row stride of Xc: 16 ceil(d/16) + 1 (odd: spreads LDS banks)
   int pst;                     // stride of params per slot
   int gps;                     // stride of per-unit gradient partials (d + 2)
   int ngu;                     // gradient partial units per slot
@@ -40,7 +39,6 @@ struct DevBatch {
                                //                 gradient's distance sums)
   double* Y;                   // B x Npad        (y - mean(X), zero padded)
   double* K;                   // B x mat
-  double* KF;                  // B x mat
   double* Lw;                  // B x mat
   double* Linv;                // B x mat
   double* Mt;                  // B x mat

@@ -2,7 +2,7 @@
 //
 // Algorithm (restating GaussianProcesses.jl v0.12.4 update_cK!/update_mll!/update_dmll!/predict_f
 // as used by examples/maximal_coordinates/*noise.jl; see DESIGN.md for the kernel map):
-//   K, Kf = sf2 * exp(-r/2) (+ (sn2 + eps) I),  r_ij = sum_p il2_p * dist_p(x_i, x_j)  (gram)
+//   K = sf2 * exp(-r/2) + (sn2 + eps) I,  r_ij = sum_p il2_p * dist_p(x_i, x_j)          (gram)
 //   recursive Cholesky + triangular inverse on 64x64 tiles (host recursion, gprx_api.hip):
 //     [A11 .; A21 A22]: rec(A11) -> L11, L11^-1 ; L21 = A21 L11^-T (TRSM) ;
 //     A22 -= L21 L21^T (SYRK) ; rec(A22) ; T^T = L11^-T L21^T (TT) ; L21^-1 = -L22^-1 T (LINV21)
@@ -21,6 +21,8 @@
 // Workgroup -> (slot, unit) mapping keeps every slot's units on one XCD (blocks b, b+8, ... share
 // an XCD), so the panels of a slot stay in that XCD's L2.
 #include "gprx_internal.h"
+#include <cstdlib>
+#include <vector>
 
 namespace gprx {
 
@@ -195,7 +197,7 @@ __device__ __forceinline__ void acc_zero(d4 (&acc)[WM][WN]) {
 }
 
 // ============================================================================================
-// Gram: lower tiles of K (with noise) and Kf (without).  grid = B * ntl, 256 threads, each thread
+// Gram: lower tiles of K (noise on the diagonal).  grid = B * ntl, 256 threads, each thread
 // a 4x4 register block; X tiles in dynamic LDS as [p][64].
 // ============================================================================================
 __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
@@ -251,27 +253,23 @@ __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
       for (int b = 0; b < 4; ++b) rr[a][b] = rr[a][b] + sqd2(av[a], a2[a], bv[b], b2[b], mode) * w;
   }
   double* K = db.K + (size_t)slot * db.mat;
-  double* KF = db.KF + (size_t)slot * db.mat;
 #pragma unroll
   for (int b = 0; b < 4; ++b) {
     const int gj = j * TS + 4 * cb + b;
-    double kv[4], fv[4];
+    double kv[4];
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
       const int gi = i * TS + 4 * rb + a;
       if (gi >= db.N || gj >= db.N) {
-        fv[a] = 0.0;
         kv[a] = (gi == gj) ? 1.0 : 0.0;
       } else {
-        fv[a] = sf2 * exp(-rr[a][b] * 0.5);
-        kv[a] = (gi == gj) ? fv[a] + noise : fv[a];
+        const double fv = sf2 * exp(-rr[a][b] * 0.5);
+        kv[a] = (gi == gj) ? fv + noise : fv;
       }
     }
     const size_t off = (size_t)gj * db.ld + i * TS + 4 * rb;
     *(double2*)(K + off) = make_double2(kv[0], kv[1]);
     *(double2*)(K + off + 2) = make_double2(kv[2], kv[3]);
-    *(double2*)(KF + off) = make_double2(fv[0], fv[1]);
-    *(double2*)(KF + off + 2) = make_double2(fv[2], fv[3]);
   }
 }
 
@@ -733,9 +731,9 @@ __global__ __launch_bounds__(NTHR) void k_leaf(DevBatch db, int o, int n) {
   double* Mt = db.Mt + so;
   for (int k = 0; k < n; ++k) {
     const int tk = o + k, m = n - 1 - k;
-    diag_tile(db, slot, tk);
+    if (!(db.ablate & 8)) diag_tile(db, slot, tk);  // ablate bits: timing experiments only
     __syncthreads();
-    for (int t = tw; t < m; t += 2) {  // TRSM
+    for (int t = tw; t < ((db.ablate & 16) ? 0 : m); t += 2) {  // TRSM
       const int ti = tk + 1 + t;
       d4 acc[WM][WN];
       acc_zero(acc);
@@ -743,7 +741,7 @@ __global__ __launch_bounds__(NTHR) void k_leaf(DevBatch db, int o, int n) {
       acc_store(Lw + (size_t)(tk * TS + 32 * half) * ld + ti * TS, ld, acc, 1.0);
     }
     __syncthreads();
-    for (int t = tw; t < m * (m + 1) / 2; t += 2) {  // SYRK (lower tiles of the trailing block)
+    for (int t = tw; t < ((db.ablate & 16) ? 0 : m * (m + 1) / 2); t += 2) {  // SYRK (lower tiles of the trailing block)
       int a = t, c = 0;
       while (a >= m - c) {
         a -= m - c;
@@ -757,7 +755,7 @@ __global__ __launch_bounds__(NTHR) void k_leaf(DevBatch db, int o, int n) {
     }
     __syncthreads();
   }
-  for (int s = 1; s < n; ++s) {
+  for (int s = 1; s < ((db.ablate & 32) ? 0 : n); ++s) {
     for (int t = tw; t < n - s; t += 2) {
       const int tj = o + t, ti = tj + s;
       double* Xt = Mt + (size_t)(ti * TS) * ld + tj * TS + 32 * half;  // Mt[tj,ti], this wave's rows
@@ -841,7 +839,8 @@ __device__ __forceinline__ void lauum_body(const DevBatch& db) {
   const int xs = db.xs, xt = TS * xs;  // point-tile image: [64][xs], dims >= d zero
   double* xr_s = sm;                    // [2][64][xs] rows of ti, ti+1
   double* xc_s = sm + 2 * xt;           // [64][xs]    rows of tj
-  double* sp = sm + 3 * xt;        // [4][SPW]
+  double* sp = sm + 3 * xt;             // [4][SPW]
+  double* nrm = sp + 4 * SPW;           // [3][64] weighted squared norms of the staged points
   const int nt = db.nt;
   int slot, u, pr, tj;
   if (!map_block(blockIdx.x, db.B, pair_units(nt, nt, true), slot, u)) return;
@@ -866,7 +865,15 @@ __device__ __forceinline__ void lauum_body(const DevBatch& db) {
   double sf = 0.0, tr = 0.0;
   double* spw = sp + w * SPW;
   for (int e = l; e < SPW; e += 64) spw[e] = 0.0;
-  const double* KF = db.KF + so + (size_t)(tj * TS + 32 * wc) * ld + ti * TS;
+  const double* P = db.params + (size_t)slot * db.pst;
+  // weighted squared norms n_t = sum_p il2_p xc_pt^2 of the 3 x 64 staged points
+  for (int t = tid; t < 3 * TS; t += NTHR) {
+    const double* xp = sm + (size_t)t * xs;
+    double nn = 0.0;
+    for (int p = 0; p < d; ++p) nn = fma(P[p] * xp[p], xp[p], nn);
+    nrm[t] = nn;
+  }
+  __syncthreads();
   if (active && !(db.ablate & 2)) {
     double ar[WM], ac[WN][4];
 #pragma unroll
@@ -875,29 +882,49 @@ __device__ __forceinline__ void lauum_body(const DevBatch& db) {
     for (int b = 0; b < WN; ++b)
 #pragma unroll
       for (int q = 0; q < 4; ++q) ac[b][q] = al[tj * TS + 32 * wc + 16 * b + lk + 4 * q];
-    // G in place of acc
+    const double sf2 = P[d];
+    const double* xr = xr_s + wr * xt;  // [r][xs]
+    const double* nr = nrm + wr * TS;
+    const double* nc = nrm + 2 * TS + 32 * wc;
+    // il2 of the k dims this lane feeds to the distance MFMA (k = 4s + lk)
+    double wk[DMAX / 4];
+    const int KS = (d + 3) >> 2;
+#pragma unroll
+    for (int s2 = 0; s2 < DMAX / 4; ++s2) wk[s2] = (s2 < KS && 4 * s2 + lk < d) ? P[4 * s2 + lk] : 0.0;
+    // G in place of acc:  Kf recomputed from r = n_r + n_c - 2 sum_p il2_p xc_pr xc_pc (MFMA, one
+    // 16 x 16 block at a time; same centred points as the distance sums below)
 #pragma unroll
     for (int a = 0; a < WM; ++a)
 #pragma unroll
-      for (int b = 0; b < WN; ++b)
+      for (int b = 0; b < WN; ++b) {
+        d4 cr = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int s2 = 0; s2 < DMAX / 4; ++s2)
+          if (s2 < KS) {
+            const double xa = wk[s2] * xr[(16 * a + lr) * xs + 4 * s2 + lk];
+            const double xb = xc_s[(32 * wc + 16 * b + lr) * xs + 4 * s2 + lk];
+            cr = mfma(xb, xa, cr);  // cr[q] = sum_p il2 x_{p,16a+lr} x_{p,32wc+16b+lk+4q}
+          }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int r = 16 * a + lr, c = 32 * wc + 16 * b + lk + 4 * q;
           const int gi = ti * TS + r, gj = tj * TS + c;
           double G = 0.0;
           if (gi < db.N && gj < db.N && gi >= gj) {
-            const double kf = KF[(size_t)(16 * b + lk + 4 * q) * ld + r];
             const double W = ar[a] * ac[b][q] - acc[a][b][q];
             if (gi == gj) {
-              G = 0.5 * (W * kf);
+              G = 0.5 * (W * sf2);
               tr += W;
             } else {
+              const double rr = fma(-2.0, cr[q], nr[r] + nc[16 * b + lk + 4 * q]);
+              const double kf = (db.ablate & 64) ? 1.0 : sf2 * exp(-0.5 * (rr > 0.0 ? rr : 0.0));
               G = W * kf;
             }
             sf += G;
           }
           acc[a][b][q] = G;
         }
+      }
     // row sums R (row 16a + lr, all 32 columns of the wave), column sums C (column
     // 32wc + 16b + lk + 4q, all 64 rows)
     double R[WM], Cs[WN][4];
@@ -923,8 +950,7 @@ __device__ __forceinline__ void lauum_body(const DevBatch& db) {
         s += __shfl_xor(s, 8);
         Cs[b][q] = s;
       }
-    const double* xr = xr_s + wr * xt;  // [r][xs]
-    const int H = (d + 15) >> 4;
+    const int H = (db.ablate & 128) ? 0 : (d + 15) >> 4;
 #pragma unroll 1
     for (int h = 0; h < H; ++h) {
       {
@@ -1010,6 +1036,27 @@ void lauum_order_host(int nt, int* out) {
         out[2 * k + 1] = c;
         ++k;
       }
+  const char* ev = getenv("GPRX_LAUUM_ORDER");  // experiment: 1 = shuffled, 2 = long/short zig-zag
+  const int mode = ev ? atoi(ev) : 0;
+  if (mode == 1) {
+    unsigned x = 12345u;
+    for (int i = k - 1; i > 0; --i) {
+      x = x * 1664525u + 1013904223u;
+      const int j = (int)((x >> 8) % (unsigned)(i + 1));
+      for (int t = 0; t < 2; ++t) {
+        const int v = out[2 * i + t];
+        out[2 * i + t] = out[2 * j + t];
+        out[2 * j + t] = v;
+      }
+    }
+  } else if (mode == 2) {
+    std::vector<int> tmp(out, out + 2 * k);
+    for (int i = 0, lo = 0, hi = k - 1; i < k; ++i) {
+      const int src = (i & 1) ? hi-- : lo++;
+      out[2 * i] = tmp[2 * src];
+      out[2 * i + 1] = tmp[2 * src + 1];
+    }
+  }
 }
 
 // ============================================================================================
@@ -1159,7 +1206,7 @@ __global__ __launch_bounds__(NTHR) void k_pred_final(DevBatch db) {
 // launchers
 // ---------------------------------------------------------------------------------------------
 static size_t gram_lds(int d) { return (size_t)(2 * d * TS + DMAX + 4) * sizeof(double); }
-static size_t lauum_lds(int d) { return (size_t)(3 * (16 * ((d + 15) / 16) + 2) * TS + 4 * SPW) * sizeof(double); }
+static size_t lauum_lds(int d) { return (size_t)(3 * (16 * ((d + 15) / 16) + 1) * TS + 4 * SPW + 3 * TS) * sizeof(double); }
 static size_t cross_lds(int d) { return (size_t)(2 * d * TS + DMAX + 4 + TS + 16 * TS) * sizeof(double); }
 
 static void set_lds_limits() {
