@@ -640,6 +640,8 @@ int gprx_batch_run(gprx_batch* b, const double* theta, unsigned flags, double* m
     db.small_n = sn ? atoi(sn) : 8;
     const char* dv = getenv("GPRX_DIAGV");
     db.diag_variant = dv ? atoi(dv) : 1;
+    const char* lfv = getenv("GPRX_LEAFV");
+    db.leaf_variant = lfv ? atoi(lfv) : 0;
     const char* lv = getenv("GPRX_LAUUMV");
     db.lauum_variant = lv ? atoi(lv) : 1;
   }

@@ -28,6 +28,7 @@ struct DevBatch {
   int small_n;                 // (GPRX_SMALL_N)
   int lauum_variant;           // k_lauum_grad variant (env GPRX_LAUUMV; experiments)
   int diag_variant;            // 0: 4-wave k_diag, 1: one-wave k_diag_w (env GPRX_DIAGV)
+  int leaf_variant;            // k_leaf occupancy variant (env GPRX_LEAFV)
   int xs;                      // row stride of Xc: 16 ceil(d/16) + 1 (odd: spreads LDS banks)
   int pst;                     // stride of params per slot
   int gps;                     // stride of per-unit gradient partials (d + 2)

@@ -99,12 +99,28 @@ __device__ __forceinline__ double sqd2(double a, double a2, double b, double b2,
   return t * t;
 }
 
+// sqrt(p) and 1/sqrt(p) for p > 0 (normal range) by v_rsq_f64 + Newton: two steps on r = p^-1/2,
+// then one Heron step on s = p r (about 1 ulp; no library call on the pivot chain)
+__device__ __forceinline__ void sqrt_rsqrt(double p, double& s, double& r) {
+  r = __builtin_amdgcn_rsq(p);
+  r = r * fma(-0.5 * p * r, r, 1.5);
+  r = r * fma(-0.5 * p * r, r, 1.5);
+  s = p * r;
+  s = fma(0.5 * r, fma(-s, s, p), s);
+}
 // 1/p by v_rcp_f64 + two Newton steps (|error| <= 1 ulp; the reference's dpotf2 scales by 1/ajj too)
 __device__ __forceinline__ double recip(double p) {
   double r = __builtin_amdgcn_rcp(p);
   r = fma(r, fma(-p, r, 1.0), r);
   r = fma(r, fma(-p, r, 1.0), r);
   return r;
+}
+
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, lane);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -413,6 +429,194 @@ __device__ __forceinline__ void diag_tile(const DevBatch& db, int slot, int jt) 
   }
 }
 __global__ __launch_bounds__(NTHR) void k_diag(DevBatch db, int jt) { diag_tile(db, blockIdx.x, jt); }
+__device__ __forceinline__ void diag_tile_fast(const DevBatch& db, int slot, int jt);
+__global__ __launch_bounds__(NTHR) void k_diag_f(DevBatch db, int jt) { diag_tile_fast(db, blockIdx.x, jt); }
+// --------------------------------------------------------------------------------------------
+// Same leaf, blocked by 16 (4 waves): the 16x16 diagonal blocks are factored and inverted in
+// registers by wave 0 (lane = row / column, pivots and row values broadcast by readlane), the
+// panel TRSM / trailing SYRK and the off-diagonal blocks of the inverse run on the MFMA pipe from
+// an LDS image of the tile.  4 + 3 barrier-separated phases per panel instead of 128 steps.
+//   panel P (c0 = 16P):  D = chol(A_PP), Dinv = D^-1               (wave 0)
+//                        A_iP <- A_iP Dinv^T  (i > P)              (TRSM, one wave per block)
+//                        A_ij -= A_iP A_jP^T  (i >= j > P)          (SYRK)
+//   inverse:  X_PP = Dinv_P ;  X_ij = -Dinv_i sum_{k=j}^{i-1} L_ik X_kj   by sub-diagonal i - j
+// Failure semantics as diag_tile (first pivot <= 0 or NaN; continue with pivot 1).
+// 16x16x4 f64 MFMA operand maps (gfx950): A lane l = A[l&15][l>>4], B lane l = B[l>>4][l&15],
+// D lane l reg q = D[(l>>4) + 4q][l&15].
+// --------------------------------------------------------------------------------------------
+constexpr int FS = TS + 1;  // LDS column stride of the tile images
+__device__ __forceinline__ void diag_tile_fast(const DevBatch& db, int slot, int jt) {
+  __shared__ double T[TS * FS];   // T[c*FS + r] = A[r][c], then L (lower)
+  __shared__ double Xi[TS * FS];  // Xi[c*FS + r] = X[r][c] = (L^-1)[r][c]
+  __shared__ __attribute__((aligned(16))) double cbs[256];
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, lr = l & 15, lk = l >> 4;
+  const size_t ld = db.ld;
+  const double* A = db.K + (size_t)slot * db.mat + (size_t)jt * TS * ld + jt * TS;
+  for (int e = tid; e < TS * TS; e += NTHR) {
+    const int r = e & 63, c = e >> 6;
+    T[c * FS + r] = (r >= c) ? A[(size_t)c * ld + r] : 0.0;
+    Xi[c * FS + r] = 0.0;
+  }
+  __syncthreads();
+  int fail = -1;
+  double lsum = 0.0;  // wave 0: sum log l_jj
+  for (int P = 0; P < 4; ++P) {
+    const int c0 = 16 * P;
+    if (w == 0 && !(db.ablate & 256)) {
+      // ---- factor the diagonal block: lane i < 16 holds row i (a[k] = A[c0+i][c0+k]); the
+      //      scaled column j is published in LDS (cb) and read back as broadcasts ----
+      double* cb = cbs;  // scratch: column j of L during the factor, then the row-major L block
+      double a[16], ri[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) a[k] = T[(c0 + k) * FS + c0 + lr];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const double p = readlane_d(a[j], j);
+        const double pk = (p > 0.0) ? p : 1.0;
+        if (!(p > 0.0) && fail < 0) fail = c0 + j;
+        double ljj, rj;
+        sqrt_rsqrt(pk, ljj, rj);
+        ri[j] = rj;
+        a[j] = (lr > j) ? a[j] * rj : (lr == j ? ljj : 0.0);
+        if (j < 15) {
+          if (l < 16) cb[j * 16 + l] = a[j];  // column j of L (row-major scratch: cb[j*16 + i])
+          __builtin_amdgcn_wave_barrier();
+          double lk[16];
+#pragma unroll
+          for (int k = (j + 1) & ~1; k < 16; k += 2) {
+            const double2 v = *(const double2*)(cb + j * 16 + k);
+            lk[k] = v.x;
+            lk[k + 1] = v.y;
+          }
+#pragma unroll
+          for (int k = j + 1; k < 16; ++k) a[k] = fma(-a[j], lk[k], a[k]);
+        }
+      }
+      // L block row-major into the scratch (cb[i*16 + k] = L[i][k]) for the inverse's broadcasts
+      __builtin_amdgcn_wave_barrier();
+      if (l < 16) {
+#pragma unroll
+        for (int k = 0; k < 16; k += 2) *(double2*)(cb + l * 16 + k) = make_double2(a[k], a[k + 1]);
+      }
+      __builtin_amdgcn_wave_barrier();
+      // ---- inverse of the block: lane c < 16 holds column c of X (x[r] = X[r][c]) ----
+      double x[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        double Lr[16];
+#pragma unroll
+        for (int m = 0; m < (r & ~1); m += 2) {
+          const double2 v = *(const double2*)(cb + r * 16 + m);
+          Lr[m] = v.x;
+          Lr[m + 1] = v.y;
+        }
+        if (r & 1) Lr[r - 1] = cb[r * 16 + r - 1];
+        double t = (r == lr) ? 1.0 : 0.0;
+#pragma unroll
+        for (int m = 0; m < r; ++m) t = fma(-Lr[m], x[m], t);
+        x[r] = t * ri[r];
+      }
+      if (l < 16) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) T[(c0 + k) * FS + c0 + l] = (k <= l) ? a[k] : 0.0;  // row l of L_PP
+      }
+      __builtin_amdgcn_wave_barrier();
+      if (l < 16) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) Xi[(c0 + l) * FS + c0 + r] = x[r];    // column l of Dinv
+      }
+    }
+    __syncthreads();
+    // ---- TRSM: block row i > P:  A_iP <- A_iP Dinv^T   (D[r][c] = sum_k A_iP[r][k] Dinv[c][k]) ----
+    {
+      const int i = P + 1 + w;
+      if (i < 4 && !(db.ablate & 512)) {
+        d4 acc = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int k = 4 * s + lk;
+          const double av = T[(c0 + k) * FS + 16 * i + lr];   // A_iP[lr][k]
+          const double bv = Xi[(c0 + k) * FS + c0 + lr];      // B[k][j=lr] = Dinv[lr][k]
+          acc = mfma(av, bv, acc);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) T[(c0 + lr) * FS + 16 * i + lk + 4 * q] = acc[q];  // D[lk+4q][lr]
+      }
+    }
+    __syncthreads();
+    // ---- SYRK: A_ij -= A_iP A_jP^T for P < j <= i < 4 ----
+    {
+      const int m = 3 - P;  // trailing blocks per edge
+      for (int t = w; t < ((db.ablate & 512) ? 0 : m * (m + 1) / 2); t += 4) {
+        int u = t, j = 0;
+        while (u >= m - j) {
+          u -= m - j;
+          ++j;
+        }
+        const int bj = P + 1 + j, bi = bj + u;
+        d4 acc = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int k = 4 * s + lk;
+          const double av = T[(c0 + k) * FS + 16 * bi + lr];  // A_iP[lr][k]
+          const double bv = T[(c0 + k) * FS + 16 * bj + lr];  // B[k][lr] = A_jP[lr][k]
+          acc = mfma(av, bv, acc);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          double* pp = &T[(16 * bj + lr) * FS + 16 * bi + lk + 4 * q];
+          *pp = *pp - acc[q];
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // ---- off-diagonal blocks of the inverse, by sub-diagonal s = i - j ----
+  for (int sd = 1; sd < ((db.ablate & 1024) ? 1 : 4); ++sd) {
+    const int j = w, i = w + sd;
+    if (i < 4) {
+      // Y = sum_{k=j}^{i-1} L_ik X_kj
+      d4 y = (d4){0.0, 0.0, 0.0, 0.0};
+      for (int kb = j; kb < i; ++kb)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int k = 4 * s + lk;
+          const double av = T[(16 * kb + k) * FS + 16 * i + lr];    // L_ik[lr][k]
+          const double bv = Xi[(16 * j + lr) * FS + 16 * kb + k];   // X_kj[k][lr]
+          y = mfma(av, bv, y);
+        }
+      // X_ij = -Dinv_i Y ; Y's D layout (reg q = Y[lk+4q][lr]) is the B operand of k-chunk q
+      d4 x = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const double av = Xi[(16 * i + 4 * s + lk) * FS + 16 * i + lr];  // Dinv_i[lr][4s+lk]
+        x = mfma(av, y[s], x);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Xi[(16 * j + lr) * FS + 16 * i + lk + 4 * q] = -x[q];
+    }
+    __syncthreads();
+  }
+  if (w == 0) {  // fail: uniform over wave 0; sum log l_jj from the diagonal of T, one per lane
+    lsum = wave_sum(log(T[l * FS + l]));
+    if (l == 0) {
+      db.logdet_part[(size_t)slot * db.nt + jt] = lsum;
+      if (fail >= 0 && db.status[slot] == 0) {
+        db.status[slot] = 1;
+        db.info[slot] = jt * TS + fail + 1;
+      }
+    }
+  }
+  double* Li = db.Linv + (size_t)slot * db.mat + (size_t)jt * TS * ld + jt * TS;
+  double* Mj = db.Mt + (size_t)slot * db.mat + (size_t)jt * TS * ld + jt * TS;
+  for (int e = tid; e < ((db.ablate & 2048) ? 0 : TS * TS); e += NTHR) {
+    const int r = e & 63, c = e >> 6;
+    const double v = (r >= c) ? Xi[c * FS + r] : 0.0;
+    Li[(size_t)c * ld + r] = v;                              // Linv[r][c]
+    Mj[(size_t)c * ld + r] = (c >= r) ? Xi[r * FS + c] : 0.0;  // Mt[r][c] = X[c][r]
+  }
+}
+
 
 // --------------------------------------------------------------------------------------------
 // Same leaf, ONE wave per slot (no workgroup barriers on the 128-step dependency chain).
@@ -428,12 +632,6 @@ __global__ __launch_bounds__(NTHR) void k_diag(DevBatch db, int jt) { diag_tile(
 // --------------------------------------------------------------------------------------------
 constexpr int CS = 66;  // LDS row stride (16-B aligned rows)
 constexpr int DWS = 2 * TS * CS;
-__device__ __forceinline__ double readlane_d(double v, int lane) {
-  const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_readlane((int)b, lane);
-  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
-  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
 // a[q][i] -= f * v[16q + i] for the NQ live chunks (static), 8 columns at a time
 template <int NQ>
 __device__ __forceinline__ void chunk_update(double (&a)[4][16], const double* v, double f) {
@@ -721,7 +919,8 @@ __device__ __forceinline__ void acc_store_t(double* Ct, size_t ld, const d4 (&ac
       for (int q = 0; q < 4; ++q) Ct[(size_t)(16 * a + lr) * ld + 16 * b + lk + 4 * q] = sgn * acc[a][b][q];
 }
 
-__global__ __launch_bounds__(NTHR) void k_leaf(DevBatch db, int o, int n) {
+template <int V>
+__device__ __forceinline__ void leaf_body(const DevBatch& db, int o, int n) {
   const int slot = blockIdx.x;
   const int w = threadIdx.x >> 6, half = w & 1, tw = w >> 1;
   const size_t ld = db.ld, so = (size_t)slot * db.mat;
@@ -731,13 +930,13 @@ __global__ __launch_bounds__(NTHR) void k_leaf(DevBatch db, int o, int n) {
   double* Mt = db.Mt + so;
   for (int k = 0; k < n; ++k) {
     const int tk = o + k, m = n - 1 - k;
-    if (!(db.ablate & 8)) diag_tile(db, slot, tk);  // ablate bits: timing experiments only
+    if (!(db.ablate & 8)) diag_tile_fast(db, slot, tk);  // ablate bits: timing experiments only
     __syncthreads();
     for (int t = tw; t < ((db.ablate & 16) ? 0 : m); t += 2) {  // TRSM
       const int ti = tk + 1 + t;
       d4 acc[WM][WN];
       acc_zero(acc);
-      mma_64x32(acc, K + (size_t)tk * TS * ld + ti * TS, ld, Li + (size_t)tk * TS * ld + tk * TS + 32 * half, ld, TS);
+      mma_v<V>(acc, K + (size_t)tk * TS * ld + ti * TS, ld, Li + (size_t)tk * TS * ld + tk * TS + 32 * half, ld, TS);
       acc_store(Lw + (size_t)(tk * TS + 32 * half) * ld + ti * TS, ld, acc, 1.0);
     }
     __syncthreads();
@@ -750,7 +949,7 @@ __global__ __launch_bounds__(NTHR) void k_leaf(DevBatch db, int o, int n) {
       const int tj = tk + 1 + c, ti = tj + a;
       d4 acc[WM][WN];
       acc_zero(acc);
-      mma_64x32(acc, Lw + (size_t)tk * TS * ld + ti * TS, ld, Lw + (size_t)tk * TS * ld + tj * TS + 32 * half, ld, TS);
+      mma_v<V>(acc, Lw + (size_t)tk * TS * ld + ti * TS, ld, Lw + (size_t)tk * TS * ld + tj * TS + 32 * half, ld, TS);
       acc_sub(K + (size_t)(tj * TS + 32 * half) * ld + ti * TS, ld, acc);
     }
     __syncthreads();
@@ -761,17 +960,22 @@ __global__ __launch_bounds__(NTHR) void k_leaf(DevBatch db, int o, int n) {
       double* Xt = Mt + (size_t)(ti * TS) * ld + tj * TS + 32 * half;  // Mt[tj,ti], this wave's rows
       d4 acc[WM][WN];
       acc_zero(acc);
-      mma_64x32(acc, Lw + (size_t)tj * TS * ld + ti * TS, ld, Mt + (size_t)tj * TS * ld + tj * TS + 32 * half, ld, s * TS);
+      mma_v<V>(acc, Lw + (size_t)tj * TS * ld + ti * TS, ld, Mt + (size_t)tj * TS * ld + tj * TS + 32 * half, ld, s * TS);
       acc_store_t(Xt, ld, acc, 1.0);
       __threadfence_block();
       acc_zero(acc);
-      mma_64x32(acc, Li + (size_t)ti * TS * ld + ti * TS, ld, Xt, ld, TS);
+      mma_v<V>(acc, Li + (size_t)ti * TS * ld + ti * TS, ld, Xt, ld, TS);
       __threadfence_block();  // all lanes' reads of X precede the overwrite below
       acc_store(Li + (size_t)(tj * TS + 32 * half) * ld + ti * TS, ld, acc, -1.0);
       acc_store_t(Xt, ld, acc, -1.0);
     }
     __syncthreads();
   }
+}
+
+__global__ __launch_bounds__(NTHR) void k_leaf(DevBatch db, int o, int n) { leaf_body<0>(db, o, n); }
+__global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_leaf_o2(DevBatch db, int o, int n) {
+  leaf_body<2>(db, o, n);
 }
 
 // ============================================================================================
@@ -1227,10 +1431,14 @@ void launch_gram(const DevBatch& b, hipStream_t s) {
 void launch_center(const DevBatch& b, hipStream_t s) { hipLaunchKernelGGL(k_center, dim3(b.B), dim3(NTHR), 0, s, b); }
 void launch_diag(const DevBatch& b, int jt, hipStream_t s) {
   if (b.diag_variant == 1) hipLaunchKernelGGL(k_diag_w, dim3(b.B), dim3(64), 0, s, b, jt);
+  else if (b.diag_variant == 2) hipLaunchKernelGGL(k_diag_f, dim3(b.B), dim3(NTHR), 0, s, b, jt);
   else hipLaunchKernelGGL(k_diag, dim3(b.B), dim3(NTHR), 0, s, b, jt);
 }
 void launch_leaf(const DevBatch& b, int o, int n, hipStream_t s) {
-  hipLaunchKernelGGL(k_leaf, dim3(b.B), dim3(NTHR), 0, s, b, o, n);
+  switch (b.leaf_variant) {
+    case 1: hipLaunchKernelGGL(k_leaf_o2, dim3(b.B), dim3(NTHR), 0, s, b, o, n); break;
+    default: hipLaunchKernelGGL(k_leaf, dim3(b.B), dim3(NTHR), 0, s, b, o, n); break;
+  }
 }
 void launch_gemm(const DevBatch& b, const GemmGeom& g, hipStream_t s, const GemmGeom& g2) {
   int r0, c0, R, C;

@@ -236,3 +236,44 @@ def test_graph_replay_matches_direct_launches(gprx, golden_dir, monkeypatch):
         np.testing.assert_array_equal(out[0][0][k], out[1][0][k])
         np.testing.assert_array_equal(out[0][1][k], out[1][1][k])
     np.testing.assert_array_equal(out[0][1]["mu"], out[0][0]["mu"][:, :7])
+
+
+@pytest.mark.parametrize("leaf,diagv", [(1, 0), (1, 1), (1, 2), (2, 1), (4, 1), (8, 1)])
+def test_factorisation_paths_match_golden(gprx, golden_dir, monkeypatch, leaf, diagv):
+    """Every recursion leaf (fused k_leaf for 2..8 tiles, standalone 64x64 diagonal kernels
+    k_diag / k_diag_w / k_diag_f at leaf 1) gives the golden results, at N=256 (4 tiles) and
+    N=130 (ragged), and reports the same failing pivot on a non-PD slot."""
+    monkeypatch.setenv("GPRX_LEAF", str(leaf))
+    monkeypatch.setenv("GPRX_DIAGV", str(diagv))
+    c = gprx.Context(0)
+    try:
+        z = np.load(golden_dir / "p2_n256.npz")
+        X, Y, th, Xs = z["X"], z["Y"], z["theta"], z["Xs"]
+        G, N = Y.shape
+        b = gprx.GPBatch(G, X.shape[0], N, Xs.shape[1], ctx=c)
+        b.set_train(X, Y)
+        b.set_test(Xs)
+        r = b.run(np.tile(th, (G, 1)), grad=True, predict=True)
+        assert np.all(r["status"] == 0)
+        for g in range(G):
+            assert abs(r["mll"][g] - z["mll_exp"][g]) <= TOL_MLL * max(1.0, abs(z["mll_exp"][g]))
+            gs = max(1.0, np.max(np.abs(z["grad_exp"][g])))
+            assert np.max(np.abs(r["grad"][g] - z["grad_exp"][g])) <= TOL_GRAD * gs
+            assert np.max(np.abs(r["mu"][g] - z["mu_exp"][g])) <= TOL_MU * np.max(np.abs(Y[g]))
+            assert np.max(np.abs(r["var"][g] - z["var_exp"][g])) <= TOL_VAR * math.exp(2 * th[-1])
+        b.close()
+        Xr, yr = X[:, :130], Y[0, :130]
+        b = gprx.GPBatch(1, X.shape[0], 130, 9, ctx=c)
+        b.set_train(Xr, yr[None])
+        b.set_test(Xs[:, :9])
+        r = b.run(th[None], grad=True, predict=True)
+        check_slot(r, 0, Xr, yr, th, Xs[:, :9], 0)
+        b.close()
+        zn = np.load(golden_dir / "nonpd_p1.npz")
+        b = gprx.GPBatch(1, zn["X"].shape[0], zn["X"].shape[1], 0, ctx=c)
+        b.set_train(zn["X"], zn["Y"][:1])
+        r = b.run(zn["theta"][None], grad=True)
+        assert r["status"][0] == 1 and r["info"][0] == int(zn["info"])
+        b.close()
+    finally:
+        c.close()
