@@ -632,18 +632,10 @@ int gprx_batch_run(gprx_batch* b, const double* theta, unsigned flags, double* m
   {
     const char* ab = getenv("GPRX_ABLATE");  // timing experiments only; results are wrong when set
     db.ablate = ab ? atoi(ab) : 0;
-    const char* gv = getenv("GPRX_GEMMV");
-    db.gemm_variant = gv ? atoi(gv) : 2;
-    const char* gvs = getenv("GPRX_GEMMV_SMALL");
-    db.gemm_variant_small = gvs ? atoi(gvs) : db.gemm_variant;
     const char* sn = getenv("GPRX_SMALL_N");
-    db.small_n = sn ? atoi(sn) : 8;
+    db.small_n = sn ? atoi(sn) : 16;
     const char* dv = getenv("GPRX_DIAGV");
     db.diag_variant = dv ? atoi(dv) : 1;
-    const char* lfv = getenv("GPRX_LEAFV");
-    db.leaf_variant = lfv ? atoi(lfv) : 0;
-    const char* lv = getenv("GPRX_LAUUMV");
-    db.lauum_variant = lv ? atoi(lv) : 1;
   }
   const int d = db.d, B = db.B, np = d + 2;
   // hyper-parameters -> kernel parameters, exactly as SEArd / GPE derive them:

@@ -23,12 +23,9 @@ struct DevBatch {
   int M, Mpad, mt;             // test points (per slot), padded to 64, mt = Mpad/64
   int dist_mode;               // GPRX_DIST_EXPANDED / GPRX_DIST_DIRECT
   int ablate;                  // timing-only ablation bits (env GPRX_ABLATE; 0 in production)
-  int gemm_variant;            // k_gemm variant (env GPRX_GEMMV; experiments)
-  int gemm_variant_small;      // variant for recursion nodes of <= small_n tiles (GPRX_GEMMV_SMALL)
-  int small_n;                 // (GPRX_SMALL_N)
-  int lauum_variant;           // k_lauum_grad variant (env GPRX_LAUUMV; experiments)
+  int small_n;                 // recursion nodes of <= small_n tiles use the 64 x 32 pair-unit GEMM
+                               // (GPRX_SMALL_N, default 16); larger ones the 64 x 64 core
   int diag_variant;            // 0: 4-wave k_diag, 1: one-wave k_diag_w (env GPRX_DIAGV)
-  int leaf_variant;            // k_leaf occupancy variant (env GPRX_LEAFV)
   int xs;                      // row stride of Xc: 16 ceil(d/16) + 1 (odd: spreads LDS banks)
   int pst;                     // stride of params per slot
   int gps;                     // stride of per-unit gradient partials (d + 2)

@@ -198,90 +198,11 @@ __device__ __forceinline__ void mma_64x32_s1(d4 (&acc)[WM][WN], const double* __
     frag_mma(acc, f);
   }
 }
-
-// ---------------------------------------------------------------------------------------------
-// 64 x 64 wave core (k_gemm, k_lauum_grad): acc[a][b] += A(64 x K) B(64 x K)^T, same operand and
-// C maps as mma_64x32 (acc[a][b] lane l reg q = C[16a + (l&15)][16b + (l>>4) + 4q]), 16 MFMAs
-// per 8 fragment loads, two register stages in ping-pong.  ~250 VGPRs: two waves per SIMD.
-// Measured on MI355X (scratch/gemm3_bench.hip, 192 batched 1024 x 1024 panels): 70.3 TF/s at
-// K = 1024, 65.4 at K = 256, against 61.8 / 60.6 for the 64 x 32 single-stage core at 4 waves/SIMD.
-// ---------------------------------------------------------------------------------------------
-constexpr int QM = 4, QN = 4;
-struct Frag4 {
-  double a[4][QM], b[4][QN];
-};
-__device__ __forceinline__ void frag4_load(Frag4& f, const double* pa, const double* pb, size_t sa, size_t sb) {
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-#pragma unroll
-    for (int a = 0; a < QM; ++a) f.a[s][a] = pa[s * sa + 16 * a];
-#pragma unroll
-    for (int b = 0; b < QN; ++b) f.b[s][b] = pb[s * sb + 16 * b];
-  }
-}
-__device__ __forceinline__ void frag4_mma(d4 (&acc)[QM][QN], const Frag4& f) {
-#pragma unroll
-  for (int s = 0; s < 4; ++s)
-#pragma unroll
-    for (int a = 0; a < QM; ++a)
-#pragma unroll
-      for (int b = 0; b < QN; ++b) acc[a][b] = mfma(f.b[s][b], f.a[s][a], acc[a][b]);
-}
-__device__ __forceinline__ void mma_64x64(d4 (&acc)[QM][QN], const double* __restrict__ A, size_t lda,
-                                          const double* __restrict__ B, size_t ldb, int K) {
-  const int nst = __builtin_amdgcn_readfirstlane(K >> 4);  // even: K is whole 64-tiles
-  if (nst <= 0) return;
-  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
-  const double* pa = A + lr + (size_t)lk * lda;
-  const double* pb = B + lr + (size_t)lk * ldb;
-  const size_t sa = 4 * lda, sb = 4 * ldb;
-  Frag4 f0, f1;
-  frag4_load(f0, pa, pb, sa, sb);
-  for (int it = 0; it < nst; it += 2) {
-    frag4_load(f1, pa + (size_t)(it + 1) * 4 * sa, pb + (size_t)(it + 1) * 4 * sb, sa, sb);
-    frag4_mma(acc, f0);
-    const int n2 = (it + 2 < nst) ? it + 2 : nst - 1;
-    frag4_load(f0, pa + (size_t)n2 * 4 * sa, pb + (size_t)n2 * 4 * sb, sa, sb);
-    frag4_mma(acc, f1);
-  }
-}
-__device__ __forceinline__ void acc4_zero(d4 (&acc)[QM][QN]) {
-#pragma unroll
-  for (int a = 0; a < QM; ++a)
-#pragma unroll
-    for (int b = 0; b < QN; ++b) acc[a][b] = (d4){0.0, 0.0, 0.0, 0.0};
-}
-
-// Units of the 4-wave workgroups of k_gemm / k_lauum_grad: UR x UC output tiles (UR UC = 4), wave w
-// = tile (pr + w / UC, pc + w % UC).  The shape follows the op so that the four waves of a unit
-// share one K range where it varies by tile: TRSM (K grows with the column) 4 x 1, TT / LINV21 (K
-// set by the row) 1 x 4, SYRK (fixed K; lower triangle) and PREDVAR 2 x 2.
-__host__ __device__ inline void unit_shape(int op, int& UR, int& UC) {
-  UR = op == OP_TRSM ? 4 : ((op == OP_TT || op == OP_LINV21) ? 1 : 2);
-  UC = 4 / UR;
-}
-// rect R x C: ceil(R/UR) x ceil(C/UC) units; lower triangle of R x R (tri, 2 x 2 only): row pair
-// RP holds column pairs 0..RP.
-__host__ __device__ inline int quad_units(int R, int C, bool tri, int UR = 2, int UC = 2) {
-  if (tri) {
-    const int RP = (R + 1) / 2;
-    return RP * (RP + 1) / 2;
-  }
-  return ((R + UR - 1) / UR) * ((C + UC - 1) / UC);
-}
-__host__ __device__ inline int op_units(const GemmGeom& g, int nt, int mt) {
-  int r0, c0, R, C, UR, UC;
-  bool tri;
-  op_rect(g, nt, mt, r0, c0, R, C, tri);
-  unit_shape(g.op, UR, UC);
-  return quad_units(R, C, tri, UR, UC);
-}
-__device__ __forceinline__ void quad_tri(int u, int& rp, int& cp) {
-  int r = (int)((sqrtf(8.0f * u + 1.0f) - 1.0f) * 0.5f);
-  while ((r + 1) * (r + 2) / 2 <= u) ++r;
-  while (r * (r + 1) / 2 > u) --r;
-  rp = r;
-  cp = u - r * (r + 1) / 2;
+template <int V>
+__device__ __forceinline__ void mma_v(d4 (&acc)[WM][WN], const double* __restrict__ A, size_t lda,
+                                      const double* __restrict__ B, size_t ldb, int K) {
+  if constexpr (V == 2) mma_64x32_s1(acc, A, lda, B, ldb, K);
+  else mma_64x32(acc, A, lda, B, ldb, K);
 }
 
 __device__ __forceinline__ void acc_zero(d4 (&acc)[WM][WN]) {
@@ -834,119 +755,11 @@ __global__ __launch_bounds__(64) void k_diag_w(DevBatch db, int jt) {
 }
 
 // ============================================================================================
-// Generic batched tile GEMM of the recursion (see GemmOp).  Unit = 2 x 2 output tiles; wave
-// (wr, wc) computes tile (pr + wr, pc + wc), 64 x 64, with its own K range (triangular operands
-// are skipped at tile granularity).  Waves of tiles outside the rectangle / above the diagonal
-// return at once (no workgroup barrier in this kernel).
+// Generic batched tile GEMM of the recursion (see GemmOp).  Unit = pair of vertically adjacent
+// 64x64 output tiles in one tile column; wave (wr, wc) = tile wr of the pair, columns 32wc..+31.
 // ============================================================================================
+template <int V>
 __device__ __forceinline__ void gemm_body(const DevBatch& db, const GemmGeom& g1, const GemmGeom& g2) {
-  int r0, c0, R, C, r02, c02, R2, C2;
-  bool tri, tri2;
-  op_rect(g1, db.nt, db.mt, r0, c0, R, C, tri);
-  op_rect(g2, db.nt, db.mt, r02, c02, R2, C2, tri2);
-  const int T1 = op_units(g1, db.nt, db.mt), T2 = g2.op == OP_NONE ? 0 : op_units(g2, db.nt, db.mt);
-  int slot, u, pr, pc;
-  if (!map_block(blockIdx.x, db.B, T1 + T2, slot, u)) return;
-  const GemmGeom g = u < T1 ? g1 : g2;  // block-uniform
-  if (u >= T1) {
-    u -= T1;
-    r0 = r02; c0 = c02; R = R2; C = C2; tri = tri2;
-  }
-  const int op = g.op;
-  int UR, UC;
-  unit_shape(op, UR, UC);
-  if (tri) {
-    quad_tri(u, pr, pc);
-    pr *= 2;
-    pc *= 2;
-  } else {
-    // longest K range first (the tail of a launch is its longest units)
-    const int RU = (R + UR - 1) / UR, CU = (C + UC - 1) / UC;
-    const int pi = u / CU;
-    int pj = u - pi * CU;
-    int ri = pi;
-    switch (op) {
-      case OP_TRSM: pj = CU - 1 - pj; break;  // K grows with the column
-      case OP_TT: break;                       // K shrinks with the row
-      default: ri = RU - 1 - pi; break;        // LINV21 / PREDVAR: K grows with the row
-    }
-    pr = UR * ri;
-    pc = UC * pj;
-  }
-  const int w = threadIdx.x >> 6, wr = w / UC, wc = w - wr * UC;
-  if (pr + wr >= R || pc + wc >= C) return;  // wave-uniform: partial unit
-  if (tri && pc + wc > pr + wr) return;      // above the diagonal
-  const int ti = r0 + pr + wr, tj = c0 + pc + wc;
-  const size_t ld = db.ld, so = (size_t)slot * db.mat;
-  int kb, ke;  // K range in tiles
-  const double *A, *Bm;
-  size_t ldb = ld;
-  switch (op) {
-    case OP_TRSM: kb = g.o; ke = tj + 1; A = db.K + so; Bm = db.Linv + so; break;
-    case OP_SYRK: kb = g.o; ke = g.o + g.h; A = db.Lw + so; Bm = db.Lw + so; break;
-    case OP_TT: kb = ti; ke = g.o + g.h; A = db.Mt + so; Bm = db.Lw + so; break;
-    case OP_LINV21: kb = g.o + g.h; ke = ti + 1; A = db.Linv + so; Bm = db.Lw + so; break;
-    default:
-      kb = 0;
-      ke = ti + 1;
-      A = db.Linv + so;
-      Bm = db.KsT + (size_t)slot * db.Npad * db.Mpad;
-      ldb = db.Mpad;
-      break;
-  }
-  d4 acc[QM][QN];
-  acc4_zero(acc);
-  mma_64x64(acc, A + (size_t)kb * TS * ld + ti * TS, ld, Bm + (size_t)kb * TS * ldb + tj * TS, ldb, (ke - kb) * TS);
-  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
-  if (op == OP_PREDVAR) {
-#pragma unroll
-    for (int b = 0; b < QN; ++b)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        double v = 0.0;
-#pragma unroll
-        for (int a = 0; a < QM; ++a) v = fma(acc[a][b][q], acc[a][b][q], v);
-        v += __shfl_xor(v, 1);
-        v += __shfl_xor(v, 2);
-        v += __shfl_xor(v, 4);
-        v += __shfl_xor(v, 8);
-        if (lr == 0) db.var_part[((size_t)slot * db.nt + ti) * db.Mpad + tj * TS + 16 * b + lk + 4 * q] = v;
-      }
-    return;
-  }
-  double* Cm;
-  double sgn = 1.0;
-  switch (op) {
-    case OP_TRSM: Cm = db.Lw + so; break;
-    case OP_SYRK: Cm = db.K + so; break;
-    case OP_TT: Cm = db.Lw + so; break;
-    default: Cm = db.Linv + so; sgn = -1.0; break;
-  }
-  double* Ct = Cm + (size_t)(tj * TS) * ld + ti * TS;
-#pragma unroll
-  for (int a = 0; a < QM; ++a)
-#pragma unroll
-    for (int b = 0; b < QN; ++b)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        double* p = Ct + (size_t)(16 * b + lk + 4 * q) * ld + 16 * a + lr;
-        if (op == OP_SYRK) *p = *p - acc[a][b][q];
-        else *p = sgn * acc[a][b][q];
-      }
-  if (op == OP_LINV21) {  // Mt[tj, ti] = Linv[ti, tj]^T
-    double* Mtt = db.Mt + so + (size_t)(ti * TS) * ld + tj * TS;
-#pragma unroll
-    for (int a = 0; a < QM; ++a)
-#pragma unroll
-      for (int b = 0; b < QN; ++b)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) Mtt[(size_t)(16 * a + lr) * ld + 16 * b + lk + 4 * q] = -acc[a][b][q];
-  }
-}
-
-// Small recursion nodes: unit = 2 vertically adjacent 64 x 64 tiles, wave = 64 x 32, single-stage
-// core at 4 waves/SIMD (more, shorter units than the 2 x 2 form: better for K <= 512).
-__device__ __forceinline__ void gemm_body_pair(const DevBatch& db, const GemmGeom& g1, const GemmGeom& g2) {
   int r0, c0, R, C, r02, c02, R2, C2;
   bool tri, tri2;
   op_rect(g1, db.nt, db.mt, r0, c0, R, C, tri);
@@ -995,7 +808,7 @@ __device__ __forceinline__ void gemm_body_pair(const DevBatch& db, const GemmGeo
   }
   d4 acc[WM][WN];
   acc_zero(acc);
-  mma_64x32_s1(acc, A + (size_t)kb * TS * ld + ti * TS, ld, Bm + (size_t)kb * TS * ldb + tj * TS + 32 * wc, ldb,
+  mma_v<V>(acc, A + (size_t)kb * TS * ld + ti * TS, ld, Bm + (size_t)kb * TS * ldb + tj * TS + 32 * wc, ldb,
            (ke - kb) * TS);
   const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
   if (op == OP_PREDVAR) {
@@ -1013,6 +826,15 @@ __device__ __forceinline__ void gemm_body_pair(const DevBatch& db, const GemmGeo
         if (lr == 0)
           db.var_part[((size_t)slot * db.nt + ti) * db.Mpad + tj * TS + 32 * wc + 16 * b + lk + 4 * q] = v;
       }
+    return;
+  }
+  if (db.ablate & 4) {  // experiment: no epilogue (keep acc live)
+    double t = 0.0;
+#pragma unroll
+    for (int a = 0; a < WM; ++a)
+#pragma unroll
+      for (int b = 0; b < WN; ++b) t += acc[a][b][0] + acc[a][b][3];
+    if (t == 12345.678) db.out[0] = t;
     return;
   }
   double* Cm;
@@ -1045,11 +867,14 @@ __device__ __forceinline__ void gemm_body_pair(const DevBatch& db, const GemmGeo
   }
 }
 
-__global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_gemm_p(DevBatch db, GemmGeom g, GemmGeom g2) {
-  gemm_body_pair(db, g, g2);
+__global__ __launch_bounds__(NTHR) void k_gemm(DevBatch db, GemmGeom g, GemmGeom g2) { gemm_body<0>(db, g, g2); }
+__global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_gemm_w3(DevBatch db, GemmGeom g,
+                                                                                            GemmGeom g2) {
+  gemm_body<0>(db, g, g2);
 }
-__global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_gemm(DevBatch db, GemmGeom g, GemmGeom g2) {
-  gemm_body(db, g, g2);
+__global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_gemm_s1(DevBatch db, GemmGeom g,
+                                                                                            GemmGeom g2) {
+  gemm_body<2>(db, g, g2);
 }
 
 // ============================================================================================
@@ -1094,6 +919,7 @@ __device__ __forceinline__ void acc_store_t(double* Ct, size_t ld, const d4 (&ac
       for (int q = 0; q < 4; ++q) Ct[(size_t)(16 * a + lr) * ld + 16 * b + lk + 4 * q] = sgn * acc[a][b][q];
 }
 
+template <int V>
 __device__ __forceinline__ void leaf_body(const DevBatch& db, int o, int n) {
   const int slot = blockIdx.x;
   const int w = threadIdx.x >> 6, half = w & 1, tw = w >> 1;
@@ -1110,7 +936,7 @@ __device__ __forceinline__ void leaf_body(const DevBatch& db, int o, int n) {
       const int ti = tk + 1 + t;
       d4 acc[WM][WN];
       acc_zero(acc);
-      mma_64x32(acc, K + (size_t)tk * TS * ld + ti * TS, ld, Li + (size_t)tk * TS * ld + tk * TS + 32 * half, ld, TS);
+      mma_v<V>(acc, K + (size_t)tk * TS * ld + ti * TS, ld, Li + (size_t)tk * TS * ld + tk * TS + 32 * half, ld, TS);
       acc_store(Lw + (size_t)(tk * TS + 32 * half) * ld + ti * TS, ld, acc, 1.0);
     }
     __syncthreads();
@@ -1123,7 +949,7 @@ __device__ __forceinline__ void leaf_body(const DevBatch& db, int o, int n) {
       const int tj = tk + 1 + c, ti = tj + a;
       d4 acc[WM][WN];
       acc_zero(acc);
-      mma_64x32(acc, Lw + (size_t)tk * TS * ld + ti * TS, ld, Lw + (size_t)tk * TS * ld + tj * TS + 32 * half, ld, TS);
+      mma_v<V>(acc, Lw + (size_t)tk * TS * ld + ti * TS, ld, Lw + (size_t)tk * TS * ld + tj * TS + 32 * half, ld, TS);
       acc_sub(K + (size_t)(tj * TS + 32 * half) * ld + ti * TS, ld, acc);
     }
     __syncthreads();
@@ -1134,11 +960,11 @@ __device__ __forceinline__ void leaf_body(const DevBatch& db, int o, int n) {
       double* Xt = Mt + (size_t)(ti * TS) * ld + tj * TS + 32 * half;  // Mt[tj,ti], this wave's rows
       d4 acc[WM][WN];
       acc_zero(acc);
-      mma_64x32(acc, Lw + (size_t)tj * TS * ld + ti * TS, ld, Mt + (size_t)tj * TS * ld + tj * TS + 32 * half, ld, s * TS);
+      mma_v<V>(acc, Lw + (size_t)tj * TS * ld + ti * TS, ld, Mt + (size_t)tj * TS * ld + tj * TS + 32 * half, ld, s * TS);
       acc_store_t(Xt, ld, acc, 1.0);
       __threadfence_block();
       acc_zero(acc);
-      mma_64x32(acc, Li + (size_t)ti * TS * ld + ti * TS, ld, Xt, ld, TS);
+      mma_v<V>(acc, Li + (size_t)ti * TS * ld + ti * TS, ld, Xt, ld, TS);
       __threadfence_block();  // all lanes' reads of X precede the overwrite below
       acc_store(Li + (size_t)(tj * TS + 32 * half) * ld + ti * TS, ld, acc, -1.0);
       acc_store_t(Xt, ld, acc, -1.0);
@@ -1147,7 +973,10 @@ __device__ __forceinline__ void leaf_body(const DevBatch& db, int o, int n) {
   }
 }
 
-__global__ __launch_bounds__(NTHR) void k_leaf(DevBatch db, int o, int n) { leaf_body(db, o, n); }
+__global__ __launch_bounds__(NTHR) void k_leaf(DevBatch db, int o, int n) { leaf_body<0>(db, o, n); }
+__global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_leaf_o2(DevBatch db, int o, int n) {
+  leaf_body<2>(db, o, n);
+}
 
 // ============================================================================================
 // alpha = L^-T (L^-1 y).  phase 0: z = Linv y ; phase 1: alpha = Mt z.   grid = B * nt
@@ -1207,92 +1036,91 @@ __device__ __forceinline__ void dma_tile(double* lds, const double* src, int ndb
   }
 }
 constexpr int SPW = DMAX + 2;  // per-wave partial row: S_p (d), S_f, T
-// Unit = 2 x 2 tiles (pr, pr+1) x (pc, pc+1) of the lower triangle; wave (wr, wc) = tile
-// (pr + wr, pc + wc) if on or below the diagonal.  LDS: the unit's four point tiles (raw [64][xs]
-// images, LDS-DMA before the MFMA loop), per-wave partials, the points' weighted norms, alpha and
-// il2.
+template <int V>
 __device__ __forceinline__ void lauum_body(const DevBatch& db) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int d = db.d, tid = threadIdx.x, w = tid >> 6, wr = w >> 1, wc = w & 1;
   const int xs = db.xs, xt = TS * xs;  // point-tile image: [64][xs], dims >= d zero
-  double* xr_s = sm;                    // [2][64][xs] rows of tiles pr, pr+1
-  double* xc_s = sm + 2 * xt;           // [2][64][xs] rows of tiles pc, pc+1
-  double* sp = sm + 4 * xt;             // [4][SPW]
-  double* nrm = sp + 4 * SPW;           // [4][64] weighted squared norms (tiles pr, pr+1, pc, pc+1)
-  double* als = nrm + 4 * TS;           // [4][64] alpha of the same points
-  double* wl = als + 4 * TS;            // [DMAX] il2
+  double* xr_s = sm;                    // [2][64][xs] rows of ti, ti+1
+  double* xc_s = sm + 2 * xt;           // [64][xs]    rows of tj
+  double* sp = sm + 3 * xt;             // [4][SPW]
+  double* nrm = sp + 4 * SPW;           // [3][64] weighted squared norms of the staged points
   const int nt = db.nt;
-  int slot, u;
-  if (!map_block(blockIdx.x, db.B, db.ngu, slot, u)) return;
-  const int pr = db.lauum_order[2 * u], pc = db.lauum_order[2 * u + 1];  // longest K range first
+  int slot, u, pr, tj;
+  if (!map_block(blockIdx.x, db.B, pair_units(nt, nt, true), slot, u)) return;
+  pr = db.lauum_order[2 * u];  // units sorted by first row (longest K range first)
+  tj = db.lauum_order[2 * u + 1];
   const double* X = db.Xc + (size_t)slot * db.Npad * xs;
   const double* al = db.alpha + (size_t)slot * db.Npad;
   dma_tile(xr_s, X + (size_t)pr * xt, xt);
   if (pr + 1 < nt) dma_tile(xr_s + xt, X + (size_t)(pr + 1) * xt, xt);
-  dma_tile(xc_s, X + (size_t)pc * xt, xt);
-  if (pc + 1 < nt) dma_tile(xc_s + xt, X + (size_t)(pc + 1) * xt, xt);
-  const int ti = pr + wr, tj = pc + wc;
-  const bool active = ti < nt && tj <= ti;
+  dma_tile(xc_s, X + (size_t)tj * xt, xt);
+  const int ti = pr + wr;
+  const bool active = ti < nt;
   const int l = tid & 63, lr = l & 15, lk = l >> 4;
-  d4 acc[QM][QN];
-  acc4_zero(acc);
+  d4 acc[WM][WN];
+  acc_zero(acc);
   const size_t ld = db.ld, so = (size_t)slot * db.mat;
   if (active && !(db.ablate & 1))
-    mma_64x64(acc, db.Mt + so + (size_t)ti * TS * ld + ti * TS, ld, db.Mt + so + (size_t)ti * TS * ld + tj * TS, ld,
-              (nt - ti) * TS);
+    mma_v<V>(acc, db.Mt + so + (size_t)ti * TS * ld + ti * TS, ld, db.Mt + so + (size_t)ti * TS * ld + tj * TS + 32 * wc,
+             ld, (nt - ti) * TS);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA landed
   __syncthreads();                                   // ... and every other wave's
   double sf = 0.0, tr = 0.0;
   double* spw = sp + w * SPW;
   for (int e = l; e < SPW; e += 64) spw[e] = 0.0;
   const double* P = db.params + (size_t)slot * db.pst;
-  if (tid < d) wl[tid] = P[tid];
-  {  // one point per thread: weighted squared norm and alpha (points of missing tiles: 0)
-    const int t4 = tid >> 6, pt = tid & 63;
-    const int tile = (t4 < 2 ? pr : pc) + (t4 & 1);
-    const double* xp = sm + (size_t)tid * xs;
+  // weighted squared norms n_t = sum_p il2_p xc_pt^2 of the 3 x 64 staged points
+  for (int t = tid; t < 3 * TS; t += NTHR) {
+    const double* xp = sm + (size_t)t * xs;
     double nn = 0.0;
-    if (tile < nt)
-      for (int p = 0; p < d; ++p) nn = fma(P[p] * xp[p], xp[p], nn);
-    nrm[tid] = nn;
-    als[tid] = tile < nt ? al[tile * TS + pt] : 0.0;
+    for (int p = 0; p < d; ++p) nn = fma(P[p] * xp[p], xp[p], nn);
+    nrm[t] = nn;
   }
   __syncthreads();
   if (active && !(db.ablate & 2)) {
+    double ar[WM], ac[WN][4];
+#pragma unroll
+    for (int a = 0; a < WM; ++a) ar[a] = al[ti * TS + 16 * a + lr];
+#pragma unroll
+    for (int b = 0; b < WN; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) ac[b][q] = al[tj * TS + 32 * wc + 16 * b + lk + 4 * q];
     const double sf2 = P[d];
     const double* xr = xr_s + wr * xt;  // [r][xs]
-    const double* xc = xc_s + wc * xt;  // [c][xs]
     const double* nr = nrm + wr * TS;
-    const double* nc = nrm + (2 + wc) * TS;
-    const double* ar = als + wr * TS;
-    const double* ac = als + (2 + wc) * TS;
+    const double* nc = nrm + 2 * TS + 32 * wc;
+    // il2 of the k dims this lane feeds to the distance MFMA (k = 4s + lk)
+    double wk[DMAX / 4];
     const int KS = (d + 3) >> 2;
+#pragma unroll
+    for (int s2 = 0; s2 < DMAX / 4; ++s2) wk[s2] = (s2 < KS && 4 * s2 + lk < d) ? P[4 * s2 + lk] : 0.0;
     // G in place of acc:  Kf recomputed from r = n_r + n_c - 2 sum_p il2_p xc_pr xc_pc (MFMA, one
-    // 16 x 16 block at a time; the same centred points as the distance sums below)
+    // 16 x 16 block at a time; same centred points as the distance sums below)
 #pragma unroll
-    for (int a = 0; a < QM; ++a)
+    for (int a = 0; a < WM; ++a)
 #pragma unroll
-      for (int b = 0; b < QN; ++b) {
+      for (int b = 0; b < WN; ++b) {
         d4 cr = (d4){0.0, 0.0, 0.0, 0.0};
-#pragma unroll 4
-        for (int s2 = 0; s2 < KS; ++s2) {
-          const int k = 4 * s2 + lk;
-          const double xa = wl[k < d ? k : 0] * xr[(16 * a + lr) * xs + k];  // xr = 0 for k >= d
-          const double xb = xc[(16 * b + lr) * xs + k];
-          cr = mfma(xb, xa, cr);  // cr[q] = sum_p il2 x_{p,16a+lr} x_{p,16b+lk+4q}
-        }
+#pragma unroll
+        for (int s2 = 0; s2 < DMAX / 4; ++s2)
+          if (s2 < KS) {
+            const double xa = wk[s2] * xr[(16 * a + lr) * xs + 4 * s2 + lk];
+            const double xb = xc_s[(32 * wc + 16 * b + lr) * xs + 4 * s2 + lk];
+            cr = mfma(xb, xa, cr);  // cr[q] = sum_p il2 x_{p,16a+lr} x_{p,32wc+16b+lk+4q}
+          }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const int r = 16 * a + lr, c = 16 * b + lk + 4 * q;
+          const int r = 16 * a + lr, c = 32 * wc + 16 * b + lk + 4 * q;
           const int gi = ti * TS + r, gj = tj * TS + c;
           double G = 0.0;
           if (gi < db.N && gj < db.N && gi >= gj) {
-            const double W = ar[r] * ac[c] - acc[a][b][q];
+            const double W = ar[a] * ac[b][q] - acc[a][b][q];
             if (gi == gj) {
               G = 0.5 * (W * sf2);
               tr += W;
             } else {
-              const double rr = fma(-2.0, cr[q], nr[r] + nc[c]);
+              const double rr = fma(-2.0, cr[q], nr[r] + nc[16 * b + lk + 4 * q]);
               const double kf = (db.ablate & 64) ? 1.0 : sf2 * exp(-0.5 * (rr > 0.0 ? rr : 0.0));
               G = W * kf;
             }
@@ -1301,14 +1129,14 @@ __device__ __forceinline__ void lauum_body(const DevBatch& db) {
           acc[a][b][q] = G;
         }
       }
-    // row sums R (row 16a + lr over the tile's 64 columns), column sums C (column 16b + lk + 4q
-    // over the 64 rows)
-    double R[QM], Cs[QN][4];
+    // row sums R (row 16a + lr, all 32 columns of the wave), column sums C (column
+    // 32wc + 16b + lk + 4q, all 64 rows)
+    double R[WM], Cs[WN][4];
 #pragma unroll
-    for (int a = 0; a < QM; ++a) {
+    for (int a = 0; a < WM; ++a) {
       double s = 0.0;
 #pragma unroll
-      for (int b = 0; b < QN; ++b)
+      for (int b = 0; b < WN; ++b)
 #pragma unroll
         for (int q = 0; q < 4; ++q) s += acc[a][b][q];
       s += __shfl_xor(s, 16);
@@ -1316,7 +1144,7 @@ __device__ __forceinline__ void lauum_body(const DevBatch& db) {
       R[a] = s;
     }
 #pragma unroll
-    for (int b = 0; b < QN; ++b)
+    for (int b = 0; b < WN; ++b)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         double s = (acc[0][b][q] + acc[1][b][q]) + (acc[2][b][q] + acc[3][b][q]);
@@ -1329,53 +1157,55 @@ __device__ __forceinline__ void lauum_body(const DevBatch& db) {
     const int H = (db.ablate & 128) ? 0 : (d + 15) >> 4;
 #pragma unroll 1
     for (int h = 0; h < H; ++h) {
-      // A operand: x of column point c = 16b + 4q + lk, dimension pA = 16h + lr
-      const int pA = 16 * h + lr;
-      double xa[QN][4];
-      double t2 = 0.0;  // sum_c x_{pA,c}^2 C_c over this lane's 16 columns
+      {
+        // A operand: x of column point c = 32wc + 16b + 4q + lk, dimension pA = 16h + lr
+        const int pA = 16 * h + lr;
+        double xa[WN][4];
+        double t2 = 0.0;  // sum_c x_{pA,c}^2 C_c over this lane's 8 columns
 #pragma unroll
-      for (int b = 0; b < QN; ++b)
+        for (int b = 0; b < WN; ++b)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          xa[b][q] = xc[(16 * b + 4 * q + lk) * xs + pA];
-          t2 = fma(xa[b][q] * xa[b][q], Cs[b][q], t2);
+          for (int q = 0; q < 4; ++q) {
+            xa[b][q] = xc_s[(32 * wc + 16 * b + 4 * q + lk) * xs + pA];
+            t2 = fma(xa[b][q] * xa[b][q], Cs[b][q], t2);
+          }
+        double t13[4] = {0.0, 0.0, 0.0, 0.0};  // dims p = 16h + lk + 4q'
+#pragma unroll
+        for (int a = 0; a < WM; ++a) {
+          d4 Q = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+          for (int b = 0; b < WN; ++b)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) Q = mfma(xa[b][q], acc[a][b][q], Q);
+          // lane: row r = 16a + lr; Q[q'] = Q[r][16h + lk + 4q']
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) {
+            const double x = xr[(16 * a + lr) * xs + 16 * h + lk + 4 * qq];
+            t13[qq] = fma(x, fma(x, R[a], -2.0 * Q[qq]), t13[qq]);
+          }
         }
-      double t13[4] = {0.0, 0.0, 0.0, 0.0};  // dims p = 16h + lk + 4q'
-#pragma unroll
-      for (int a = 0; a < QM; ++a) {
-        d4 Q = (d4){0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int b = 0; b < QN; ++b)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) Q = mfma(xa[b][q], acc[a][b][q], Q);
-        // lane: row r = 16a + lr; Q[q'] = Q[r][16h + lk + 4q']
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq) {
-          const double x = xr[(16 * a + lr) * xs + 16 * h + lk + 4 * qq];
-          t13[qq] = fma(x, fma(x, R[a], -2.0 * Q[qq]), t13[qq]);
+          double s = t13[qq];
+          s += __shfl_xor(s, 1);
+          s += __shfl_xor(s, 2);
+          s += __shfl_xor(s, 4);
+          s += __shfl_xor(s, 8);
+          t13[qq] = s;
         }
-      }
+        t2 += __shfl_xor(t2, 16);
+        t2 += __shfl_xor(t2, 32);
+        if (lr == 0) {
 #pragma unroll
-      for (int qq = 0; qq < 4; ++qq) {
-        double s = t13[qq];
-        s += __shfl_xor(s, 1);
-        s += __shfl_xor(s, 2);
-        s += __shfl_xor(s, 4);
-        s += __shfl_xor(s, 8);
-        t13[qq] = s;
-      }
-      t2 += __shfl_xor(t2, 16);
-      t2 += __shfl_xor(t2, 32);
-      if (lr == 0) {
-#pragma unroll
-        for (int qq = 0; qq < 4; ++qq) {
-          const int p = 16 * h + lk + 4 * qq;
-          if (p < d) spw[p] = t13[qq];
+          for (int qq = 0; qq < 4; ++qq) {
+            const int p = 16 * h + lk + 4 * qq;
+            if (p < d) spw[p] = t13[qq];
+          }
         }
+        __builtin_amdgcn_wave_barrier();
+        if (lk == 0 && pA < d) spw[pA] += t2;
+        __builtin_amdgcn_wave_barrier();
       }
-      __builtin_amdgcn_wave_barrier();
-      if (lk == 0 && pA < d) spw[pA] += t2;
-      __builtin_amdgcn_wave_barrier();
     }
   }
   sf = wave_sum(sf);
@@ -1389,20 +1219,48 @@ __device__ __forceinline__ void lauum_body(const DevBatch& db) {
   for (int e = tid; e < d + 2; e += NTHR)
     out[e] = ((sp[e] + sp[SPW + e]) + sp[2 * SPW + e]) + sp[3 * SPW + e];
 }
-__global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_lauum_grad(DevBatch db) {
-  lauum_body(db);
+__global__ __launch_bounds__(NTHR) void k_lauum_grad(DevBatch db) { lauum_body<0>(db); }
+__global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_lauum_grad_w3(DevBatch db) {
+  lauum_body<0>(db);
 }
-int lauum_units(int nt) { return quad_units(nt, nt, true); }
+__global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_lauum_grad_s1(DevBatch db) {
+  lauum_body<2>(db);
+}
+__global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_lauum_grad_o4(DevBatch db) {
+  lauum_body<2>(db);
+}
+int lauum_units(int nt) { return pair_units(nt, nt, true); }
 void lauum_order_host(int nt, int* out) {
-  // (first row, first column) of every 2 x 2-tile unit of the lower triangle, by row pair: the
-  // K range [row, nt) shrinks down the list (longest first)
+  // (first row, column) of every tile-pair unit of the lower triangle, sorted by first row
   int k = 0;
-  for (int rp = 0; 2 * rp < nt; ++rp)
-    for (int cp = 0; cp <= rp; ++cp) {
-      out[2 * k] = 2 * rp;
-      out[2 * k + 1] = 2 * cp;
-      ++k;
+  for (int r = 0; r < nt; ++r)
+    for (int c = 0; c <= r; ++c)
+      if (((r - c) & 1) == 0) {
+        out[2 * k] = r;
+        out[2 * k + 1] = c;
+        ++k;
+      }
+  const char* ev = getenv("GPRX_LAUUM_ORDER");  // experiment: 1 = shuffled, 2 = long/short zig-zag
+  const int mode = ev ? atoi(ev) : 0;
+  if (mode == 1) {
+    unsigned x = 12345u;
+    for (int i = k - 1; i > 0; --i) {
+      x = x * 1664525u + 1013904223u;
+      const int j = (int)((x >> 8) % (unsigned)(i + 1));
+      for (int t = 0; t < 2; ++t) {
+        const int v = out[2 * i + t];
+        out[2 * i + t] = out[2 * j + t];
+        out[2 * j + t] = v;
+      }
     }
+  } else if (mode == 2) {
+    std::vector<int> tmp(out, out + 2 * k);
+    for (int i = 0, lo = 0, hi = k - 1; i < k; ++i) {
+      const int src = (i & 1) ? hi-- : lo++;
+      out[2 * i] = tmp[2 * src];
+      out[2 * i + 1] = tmp[2 * src + 1];
+    }
+  }
 }
 
 // ============================================================================================
@@ -1552,9 +1410,7 @@ __global__ __launch_bounds__(NTHR) void k_pred_final(DevBatch db) {
 // launchers
 // ---------------------------------------------------------------------------------------------
 static size_t gram_lds(int d) { return (size_t)(2 * d * TS + DMAX + 4) * sizeof(double); }
-static size_t lauum_lds(int d) {
-  return (size_t)(4 * (16 * ((d + 15) / 16) + 1) * TS + 4 * SPW + 8 * TS + DMAX) * sizeof(double);
-}
+static size_t lauum_lds(int d) { return (size_t)(3 * (16 * ((d + 15) / 16) + 1) * TS + 4 * SPW + 3 * TS) * sizeof(double); }
 static size_t cross_lds(int d) { return (size_t)(2 * d * TS + DMAX + 4 + TS + 16 * TS) * sizeof(double); }
 
 static void set_lds_limits() {
@@ -1562,7 +1418,9 @@ static void set_lds_limits() {
   if (done) return;
   done = true;
   (void)hipFuncSetAttribute((const void*)k_gram, hipFuncAttributeMaxDynamicSharedMemorySize, (int)gram_lds(DMAX));
-  (void)hipFuncSetAttribute((const void*)k_lauum_grad, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lauum_lds(DMAX));
+  for (const void* f : {(const void*)k_lauum_grad, (const void*)k_lauum_grad_w3, (const void*)k_lauum_grad_s1,
+                        (const void*)k_lauum_grad_o4})
+    (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lauum_lds(DMAX));
   (void)hipFuncSetAttribute((const void*)k_pred_cross, hipFuncAttributeMaxDynamicSharedMemorySize, (int)cross_lds(DMAX));
 }
 
@@ -1577,31 +1435,40 @@ void launch_diag(const DevBatch& b, int jt, hipStream_t s) {
   else hipLaunchKernelGGL(k_diag, dim3(b.B), dim3(NTHR), 0, s, b, jt);
 }
 void launch_leaf(const DevBatch& b, int o, int n, hipStream_t s) {
-  hipLaunchKernelGGL(k_leaf, dim3(b.B), dim3(NTHR), 0, s, b, o, n);
+  switch (b.leaf_variant) {
+    case 1: hipLaunchKernelGGL(k_leaf_o2, dim3(b.B), dim3(NTHR), 0, s, b, o, n); break;
+    default: hipLaunchKernelGGL(k_leaf, dim3(b.B), dim3(NTHR), 0, s, b, o, n); break;
+  }
 }
 void launch_gemm(const DevBatch& b, const GemmGeom& g, hipStream_t s, const GemmGeom& g2) {
-  if (g.op != OP_PREDVAR && g.n <= b.small_n) {  // small node: pair units, 64 x 32 waves
-    int r0, c0, R, C;
-    bool tri;
-    op_rect(g, b.nt, b.mt, r0, c0, R, C, tri);
-    int T = pair_units(R, C, tri);
-    if (g2.op != OP_NONE) {
-      op_rect(g2, b.nt, b.mt, r0, c0, R, C, tri);
-      T += pair_units(R, C, tri);
-    }
-    hipLaunchKernelGGL(k_gemm_p, dim3(grid_blocks(b.B, T)), dim3(NTHR), 0, s, b, g, g2);
-    return;
+  int r0, c0, R, C;
+  bool tri;
+  op_rect(g, b.nt, b.mt, r0, c0, R, C, tri);
+  int T = pair_units(R, C, tri);
+  if (g2.op != OP_NONE) {
+    op_rect(g2, b.nt, b.mt, r0, c0, R, C, tri);
+    T += pair_units(R, C, tri);
   }
-  int T = op_units(g, b.nt, b.mt);
-  if (g2.op != OP_NONE) T += op_units(g2, b.nt, b.mt);
-  hipLaunchKernelGGL(k_gemm, dim3(grid_blocks(b.B, T)), dim3(NTHR), 0, s, b, g, g2);
+  const dim3 grid(grid_blocks(b.B, T));
+  const int variant = (g.op != OP_PREDVAR && g.n <= b.small_n) ? b.gemm_variant_small : b.gemm_variant;
+  switch (variant) {
+    case 1: hipLaunchKernelGGL(k_gemm_w3, grid, dim3(NTHR), 0, s, b, g, g2); break;
+    case 2: hipLaunchKernelGGL(k_gemm_s1, grid, dim3(NTHR), 0, s, b, g, g2); break;
+    default: hipLaunchKernelGGL(k_gemm, grid, dim3(NTHR), 0, s, b, g, g2); break;
+  }
 }
 void launch_alpha(const DevBatch& b, hipStream_t s, int phase) {
   hipLaunchKernelGGL(k_alpha, dim3(grid_blocks(b.B, b.nt)), dim3(NTHR), 0, s, b, phase);
 }
 void launch_lauum_grad(const DevBatch& b, hipStream_t s) {
   set_lds_limits();
-  hipLaunchKernelGGL(k_lauum_grad, dim3(grid_blocks(b.B, lauum_units(b.nt))), dim3(NTHR), lauum_lds(b.d), s, b);
+  const dim3 grid(grid_blocks(b.B, lauum_units(b.nt)));
+  switch (b.lauum_variant) {
+    case 1: hipLaunchKernelGGL(k_lauum_grad_w3, grid, dim3(NTHR), lauum_lds(b.d), s, b); break;
+    case 2: hipLaunchKernelGGL(k_lauum_grad_s1, grid, dim3(NTHR), lauum_lds(b.d), s, b); break;
+    case 3: hipLaunchKernelGGL(k_lauum_grad_o4, grid, dim3(NTHR), lauum_lds(b.d), s, b); break;
+    default: hipLaunchKernelGGL(k_lauum_grad, grid, dim3(NTHR), lauum_lds(b.d), s, b); break;
+  }
 }
 void launch_finalize(const DevBatch& b, int want_grad, hipStream_t s) {
   hipLaunchKernelGGL(k_finalize, dim3(b.B), dim3(NTHR), 0, s, b, want_grad);
