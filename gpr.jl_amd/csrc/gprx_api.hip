@@ -632,6 +632,8 @@ int gprx_batch_run(gprx_batch* b, const double* theta, unsigned flags, double* m
   {
     const char* ab = getenv("GPRX_ABLATE");  // timing experiments only; results are wrong when set
     db.ablate = ab ? atoi(ab) : 0;
+    const char* dl = getenv("GPRX_DELAY");
+    db.delay = dl ? atoi(dl) : 0;
     const char* sn = getenv("GPRX_SMALL_N");
     db.small_n = sn ? atoi(sn) : 16;
     const char* dv = getenv("GPRX_DIAGV");

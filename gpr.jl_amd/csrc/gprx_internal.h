@@ -23,6 +23,8 @@ struct DevBatch {
   int M, Mpad, mt;             // test points (per slot), padded to 64, mt = Mpad/64
   int dist_mode;               // GPRX_DIST_EXPANDED / GPRX_DIST_DIRECT
   int ablate;                  // timing-only ablation bits (env GPRX_ABLATE; 0 in production)
+  int delay;                   // lauum: s_sleep count for the second resident workgroup of a CU in the
+                               // first dispatch round (desynchronises co-resident epilogues)
   int small_n;                 // recursion nodes of <= small_n tiles use the 64 x 32 pair-unit GEMM
                                // (GPRX_SMALL_N, default 16); larger ones the 64 x 64 core
   int diag_variant;            // 0: 4-wave k_diag, 1: one-wave k_diag_w (env GPRX_DIAGV)

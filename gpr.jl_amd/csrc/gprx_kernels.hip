@@ -269,12 +269,18 @@ __host__ __device__ inline int quad_units(int R, int C, bool tri, int UR = 2, in
   }
   return ((R + UR - 1) / UR) * ((C + UC - 1) / UC);
 }
+// Triangular-K ops are folded: a workgroup computes the unit with the longest K range and then
+// its mirror along the K-varying dimension (TRSM: columns; TT, LINV21, PREDVAR: rows), so every
+// workgroup carries about the same K (measured 58.7 -> 67.4 TF/s on a TRSM-shaped launch,
+// scratch/gemm3_bench.hip).
 __host__ __device__ inline int op_units(const GemmGeom& g, int nt, int mt) {
   int r0, c0, R, C, UR, UC;
   bool tri;
   op_rect(g, nt, mt, r0, c0, R, C, tri);
   unit_shape(g.op, UR, UC);
-  return quad_units(R, C, tri, UR, UC);
+  if (tri || g.op == OP_SYRK) return quad_units(R, C, tri, UR, UC);
+  const int RU = (R + UR - 1) / UR, CU = (C + UC - 1) / UC;
+  return g.op == OP_TRSM ? RU * ((CU + 1) / 2) : ((RU + 1) / 2) * CU;
 }
 __device__ __forceinline__ void quad_tri(int u, int& rp, int& cp) {
   int r = (int)((sqrtf(8.0f * u + 1.0f) - 1.0f) * 0.5f);
@@ -839,44 +845,9 @@ __global__ __launch_bounds__(64) void k_diag_w(DevBatch db, int jt) {
 // are skipped at tile granularity).  Waves of tiles outside the rectangle / above the diagonal
 // return at once (no workgroup barrier in this kernel).
 // ============================================================================================
-__device__ __forceinline__ void gemm_body(const DevBatch& db, const GemmGeom& g1, const GemmGeom& g2) {
-  int r0, c0, R, C, r02, c02, R2, C2;
-  bool tri, tri2;
-  op_rect(g1, db.nt, db.mt, r0, c0, R, C, tri);
-  op_rect(g2, db.nt, db.mt, r02, c02, R2, C2, tri2);
-  const int T1 = op_units(g1, db.nt, db.mt), T2 = g2.op == OP_NONE ? 0 : op_units(g2, db.nt, db.mt);
-  int slot, u, pr, pc;
-  if (!map_block(blockIdx.x, db.B, T1 + T2, slot, u)) return;
-  const GemmGeom g = u < T1 ? g1 : g2;  // block-uniform
-  if (u >= T1) {
-    u -= T1;
-    r0 = r02; c0 = c02; R = R2; C = C2; tri = tri2;
-  }
+// One 64 x 64 output tile (ti, tj) of a GemmOp on one wave.
+__device__ __forceinline__ void gemm_tile(const DevBatch& db, const GemmGeom& g, int slot, int ti, int tj) {
   const int op = g.op;
-  int UR, UC;
-  unit_shape(op, UR, UC);
-  if (tri) {
-    quad_tri(u, pr, pc);
-    pr *= 2;
-    pc *= 2;
-  } else {
-    // longest K range first (the tail of a launch is its longest units)
-    const int RU = (R + UR - 1) / UR, CU = (C + UC - 1) / UC;
-    const int pi = u / CU;
-    int pj = u - pi * CU;
-    int ri = pi;
-    switch (op) {
-      case OP_TRSM: pj = CU - 1 - pj; break;  // K grows with the column
-      case OP_TT: break;                       // K shrinks with the row
-      default: ri = RU - 1 - pi; break;        // LINV21 / PREDVAR: K grows with the row
-    }
-    pr = UR * ri;
-    pc = UC * pj;
-  }
-  const int w = threadIdx.x >> 6, wr = w / UC, wc = w - wr * UC;
-  if (pr + wr >= R || pc + wc >= C) return;  // wave-uniform: partial unit
-  if (tri && pc + wc > pr + wr) return;      // above the diagonal
-  const int ti = r0 + pr + wr, tj = c0 + pc + wc;
   const size_t ld = db.ld, so = (size_t)slot * db.mat;
   int kb, ke;  // K range in tiles
   const double *A, *Bm;
@@ -894,10 +865,20 @@ __device__ __forceinline__ void gemm_body(const DevBatch& db, const GemmGeom& g1
       ldb = db.Mpad;
       break;
   }
-  d4 acc[QM][QN];
-  acc4_zero(acc);
-  mma_64x64(acc, A + (size_t)kb * TS * ld + ti * TS, ld, Bm + (size_t)kb * TS * ldb + tj * TS, ldb, (ke - kb) * TS);
   const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  d4 acc[QM][QN];
+  if (op == OP_SYRK) {  // acc = -C, loaded before the K loop so its latency overlaps the first stage
+    const double* Cs = db.K + so + (size_t)(tj * TS) * ld + ti * TS;
+#pragma unroll
+    for (int a = 0; a < QM; ++a)
+#pragma unroll
+      for (int b = 0; b < QN; ++b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[a][b][q] = -Cs[(size_t)(16 * b + lk + 4 * q) * ld + 16 * a + lr];
+  } else {
+    acc4_zero(acc);
+  }
+  mma_64x64(acc, A + (size_t)kb * TS * ld + ti * TS, ld, Bm + (size_t)kb * TS * ldb + tj * TS, ldb, (ke - kb) * TS);
   if (op == OP_PREDVAR) {
 #pragma unroll
     for (int b = 0; b < QN; ++b)
@@ -930,17 +911,76 @@ __device__ __forceinline__ void gemm_body(const DevBatch& db, const GemmGeom& g1
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         double* p = Ct + (size_t)(16 * b + lk + 4 * q) * ld + 16 * a + lr;
-        if (op == OP_SYRK) *p = *p - acc[a][b][q];
-        else *p = sgn * acc[a][b][q];
+        *p = (op == OP_SYRK ? -1.0 : sgn) * acc[a][b][q];  // SYRK: C - L L^T = -acc
       }
-  if (op == OP_LINV21) {  // Mt[tj, ti] = Linv[ti, tj]^T
+  if (op == OP_LINV21) {  // Mt[tj, ti] = Linv[ti, tj]^T, transposed through LDS 16 rows at a time
+    // so that every store instruction writes one contiguous 512-B column segment of Mt
+    extern __shared__ __attribute__((aligned(16))) double gsm[];
+    double* tb = gsm + (threadIdx.x >> 6) * (16 * (TS + 1));  // this wave's [16][65] buffer
     double* Mtt = db.Mt + so + (size_t)(ti * TS) * ld + tj * TS;
 #pragma unroll
-    for (int a = 0; a < QM; ++a)
+    for (int a = 0; a < QM; ++a) {
 #pragma unroll
       for (int b = 0; b < QN; ++b)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) Mtt[(size_t)(16 * a + lr) * ld + 16 * b + lk + 4 * q] = -acc[a][b][q];
+        for (int q = 0; q < 4; ++q) tb[lr * (TS + 1) + 16 * b + lk + 4 * q] = -acc[a][b][q];
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int r = 0; r < 16; ++r) Mtt[(size_t)(16 * a + r) * ld + l] = tb[r * (TS + 1) + l];
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+}
+
+__device__ __forceinline__ void gemm_body(const DevBatch& db, const GemmGeom& g1, const GemmGeom& g2) {
+  int r0, c0, R, C, r02, c02, R2, C2;
+  bool tri, tri2;
+  op_rect(g1, db.nt, db.mt, r0, c0, R, C, tri);
+  op_rect(g2, db.nt, db.mt, r02, c02, R2, C2, tri2);
+  const int T1 = op_units(g1, db.nt, db.mt), T2 = g2.op == OP_NONE ? 0 : op_units(g2, db.nt, db.mt);
+  int slot, u, pr, pc;
+  if (!map_block(blockIdx.x, db.B, T1 + T2, slot, u)) return;
+  const GemmGeom g = u < T1 ? g1 : g2;  // block-uniform
+  if (u >= T1) {
+    u -= T1;
+    r0 = r02; c0 = c02; R = R2; C = C2; tri = tri2;
+  }
+  const int op = g.op;
+  int UR, UC;
+  unit_shape(op, UR, UC);
+  int np = 1, pr2 = 0, pc2 = 0;  // second (folded) unit
+  if (tri) {
+    quad_tri(u, pr, pc);
+    pr *= 2;
+    pc *= 2;
+  } else {
+    const int RU = (R + UR - 1) / UR, CU = (C + UC - 1) / UC;
+    if (op == OP_SYRK) {
+      pr = UR * (u / CU);
+      pc = UC * (u % CU);
+    } else if (op == OP_TRSM) {  // K grows with the column: fold columns
+      const int nf = (CU + 1) / 2, pi = u / nf, f = u - pi * nf;
+      pr = pr2 = UR * pi;
+      pc = UC * (CU - 1 - f);
+      pc2 = UC * f;
+      np = (CU - 1 - f != f) ? 2 : 1;
+    } else {  // fold rows; TT: K shrinks with the row, LINV21 / PREDVAR: K grows with the row
+      const int nf = (RU + 1) / 2, f = u / CU, pj = u - f * CU;
+      const int lo = f, hi = RU - 1 - f;
+      pr = UR * (op == OP_TT ? lo : hi);
+      pr2 = UR * (op == OP_TT ? hi : lo);
+      pc = pc2 = UC * pj;
+      np = (lo != hi) ? 2 : 1;
+    }
+  }
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), wr = w / UC, wc = w - wr * UC;
+#pragma unroll 1
+  for (int pass = 0; pass < np; ++pass) {
+    const int ur = pass ? pr2 : pr, uc = pass ? pc2 : pc;
+    if (ur + wr >= R || uc + wc >= C) continue;  // wave-uniform: partial unit
+    if (tri && uc + wc > ur + wr) continue;      // above the diagonal
+    // wave-uniform tile indices in SGPRs (the 64 x 64 core needs every VGPR)
+    gemm_tile(db, g, slot, __builtin_amdgcn_readfirstlane(r0 + ur + wr), __builtin_amdgcn_readfirstlane(c0 + uc + wc));
   }
 }
 
@@ -1225,6 +1265,8 @@ __device__ __forceinline__ void lauum_body(const DevBatch& db) {
   int slot, u;
   if (!map_block(blockIdx.x, db.B, db.ngu, slot, u)) return;
   const int pr = db.lauum_order[2 * u], pc = db.lauum_order[2 * u + 1];  // longest K range first
+  if (db.delay > 0 && (blockIdx.x >> 8) == 1)  // blocks 256..511: the second resident WG per CU
+    for (int i = 0; i < db.delay; ++i) __builtin_amdgcn_s_sleep(127);
   const double* X = db.Xc + (size_t)slot * db.Npad * xs;
   const double* al = db.alpha + (size_t)slot * db.Npad;
   dma_tile(xr_s, X + (size_t)pr * xt, xt);
@@ -1594,7 +1636,8 @@ void launch_gemm(const DevBatch& b, const GemmGeom& g, hipStream_t s, const Gemm
   }
   int T = op_units(g, b.nt, b.mt);
   if (g2.op != OP_NONE) T += op_units(g2, b.nt, b.mt);
-  hipLaunchKernelGGL(k_gemm, dim3(grid_blocks(b.B, T)), dim3(NTHR), 0, s, b, g, g2);
+  const size_t lds = (g.op == OP_LINV21 || g2.op == OP_LINV21) ? 4 * 16 * (TS + 1) * sizeof(double) : 0;
+  hipLaunchKernelGGL(k_gemm, dim3(grid_blocks(b.B, T)), dim3(NTHR), lds, s, b, g, g2);
 }
 void launch_alpha(const DevBatch& b, hipStream_t s, int phase) {
   hipLaunchKernelGGL(k_alpha, dim3(grid_blocks(b.B, b.nt)), dim3(NTHR), 0, s, b, phase);

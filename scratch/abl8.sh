@@ -1,0 +1,2 @@
+set -e
+for a in 0 64 128 192 2; do GPRX_ABLATE=$a timeout -k 10 200 python scratch/sweep.py 32 > gpurun_out/abl_$a.txt 2>&1; echo "ablate=$a $(grep -E 'lauum_grad ' gpurun_out/abl_$a.txt)"; done

@@ -96,6 +96,37 @@ KERN(k_e_4x2_db_o3, 4, 2, 1, 3)
 KERN(k_f_2x4_s1_o4, 2, 4, 0, 4)
 KERN(k_g_4x1_s1_o6, 4, 1, 0, 6)
 
+// TRSM-like: 16 x 16 output tiles per slot, unit = 4 rows x 1 column (waves = rows), K = (tj+1) 64.
+// fold = 0: units ordered by column descending (longest first); fold = 1: a unit does column j and
+// then column 15 - j (equal total K per workgroup).
+template <int FOLD>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_tri(const double* P, double* C, int T, int S) {
+  const int x = blockIdx.x & 7, q = blockIdx.x >> 3;
+  const int slot = (q / T) * 8 + x, u = q % T;
+  if (slot >= S) return;
+  const double* M = P + (size_t)slot * 2048 * 2048;
+  double* Cs = C + (size_t)slot * 1024 * 1024;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  const int CU = FOLD ? 8 : 16;
+  const int pi = u / CU, pj = u - pi * CU;
+  const int ti = 4 * pi + w;
+  for (int pass = 0; pass < (FOLD ? 2 : 1); ++pass) {
+    const int tj = FOLD ? (pass == 0 ? 15 - pj : pj) : 15 - pj;
+    d4 acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) acc[a][b] = (d4){0, 0, 0, 0};
+    core<4, 4, 1>(acc, M + 1024 + ti * 64, 2048, M + tj * 64, 2048, (tj + 1) * 64);
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) Cs[(size_t)(tj * 64 + 16 * b + lk + 4 * qq) * 1024 + ti * 64 + 16 * a + lr] = acc[a][b][qq];
+  }
+}
+
 int main() {
   const int S = 192;
   const size_t mat = 2048ull * 2048;
@@ -134,6 +165,22 @@ int main() {
       const double fl = 2.0 * 1024 * 1024 * (double)K * S;
       printf("K=%4d %-22s grid=%6d %8.3f ms %6.2f TF/s\n", K, v.name, grid, ms, fl / ms / 1e9);
     }
+  }
+  for (int fold = 0; fold < 2; ++fold) {
+    int T = fold ? 4 * 8 : 4 * 16, Sm = S;
+    const int grid = 8 * ((S + 7) / 8) * T;
+    const void* f = fold ? (const void*)k_tri<1> : (const void*)k_tri<0>;
+    void* a2[] = {&P, &C, &T, &Sm};
+    (void)hipLaunchKernel(f, dim3(grid), dim3(256), a2, 0, 0);
+    (void)hipEventRecord(e0);
+    for (int r = 0; r < 5; ++r) (void)hipLaunchKernel(f, dim3(grid), dim3(256), a2, 0, 0);
+    (void)hipEventRecord(e1);
+    (void)hipEventSynchronize(e1);
+    float ms;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    ms /= 5;
+    const double fl = 2.0 * 1024 * 64 * 64.0 * (16 * 17 / 2) * S;
+    printf("TRSM-like tri K fold=%d grid=%6d %8.3f ms %6.2f TF/s\n", fold, grid, ms, fl / ms / 1e9);
   }
   printf("err=%s\n", hipGetErrorString(hipGetLastError()));
   return 0;
