@@ -635,7 +635,7 @@ int gprx_batch_run(gprx_batch* b, const double* theta, unsigned flags, double* m
     const char* dl = getenv("GPRX_DELAY");
     db.delay = dl ? atoi(dl) : 0;
     const char* sn = getenv("GPRX_SMALL_N");
-    db.small_n = sn ? atoi(sn) : 16;
+    db.small_n = sn ? atoi(sn) : 8;
     const char* dv = getenv("GPRX_DIAGV");
     db.diag_variant = dv ? atoi(dv) : 1;
   }

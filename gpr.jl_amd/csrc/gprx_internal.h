@@ -26,7 +26,7 @@ struct DevBatch {
   int delay;                   // lauum: s_sleep count for the second resident workgroup of a CU in the
                                // first dispatch round (desynchronises co-resident epilogues)
   int small_n;                 // recursion nodes of <= small_n tiles use the 64 x 32 pair-unit GEMM
-                               // (GPRX_SMALL_N, default 16); larger ones the 64 x 64 core
+                               // (GPRX_SMALL_N, default 8); larger ones the 64 x 64 core
   int diag_variant;            // 0: 4-wave k_diag, 1: one-wave k_diag_w (env GPRX_DIAGV)
   int xs;                      // row stride of Xc: 16 ceil(d/16) + 1 (odd: spreads LDS banks)
   int pst;                     // stride of params per slot
