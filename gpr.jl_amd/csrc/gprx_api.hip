@@ -489,6 +489,7 @@ int gprx_batch_create(gprx_ctx* c, int B, int d, int N, int M_max, gprx_batch** 
   db.pst = d + 4;
   db.gps = d + 2;
   db.ngu = gprx::lauum_units(db.nt);
+  db.nlj = gprx::lauum_jobs(db.nt);
   const size_t Bs = B;
   int rc = GPRX_OK;
   auto fail = [&](int r) {
@@ -511,9 +512,9 @@ int gprx_batch_create(gprx_ctx* c, int B, int d, int N, int M_max, gprx_batch** 
   if ((rc = dalloc(b, &db.out, Bs * (d + 3)))) return fail(rc);
   if ((rc = dalloc(b, &db.status, 2 * Bs))) return fail(rc);
   db.info = db.status + Bs;
-  if ((rc = dalloc(b, &db.lauum_order, 2 * (size_t)db.ngu))) return fail(rc);
+  if ((rc = dalloc(b, &db.lauum_order, 6 * (size_t)db.nlj))) return fail(rc);
   {
-    std::vector<int> ord(2 * (size_t)db.ngu);
+    std::vector<int> ord(6 * (size_t)db.nlj);
     gprx::lauum_order_host(db.nt, ord.data());
     if (hipMemcpy(db.lauum_order, ord.data(), ord.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess)
       return fail(GPRX_DEVICE_ERROR);
@@ -632,8 +633,6 @@ int gprx_batch_run(gprx_batch* b, const double* theta, unsigned flags, double* m
   {
     const char* ab = getenv("GPRX_ABLATE");  // timing experiments only; results are wrong when set
     db.ablate = ab ? atoi(ab) : 0;
-    const char* dl = getenv("GPRX_DELAY");
-    db.delay = dl ? atoi(dl) : 0;
     const char* sn = getenv("GPRX_SMALL_N");
     db.small_n = sn ? atoi(sn) : 8;
     const char* dv = getenv("GPRX_DIAGV");

@@ -23,15 +23,14 @@ struct DevBatch {
   int M, Mpad, mt;             // test points (per slot), padded to 64, mt = Mpad/64
   int dist_mode;               // GPRX_DIST_EXPANDED / GPRX_DIST_DIRECT
   int ablate;                  // timing-only ablation bits (env GPRX_ABLATE; 0 in production)
-  int delay;                   // lauum: s_sleep count for the second resident workgroup of a CU in the
-                               // first dispatch round (desynchronises co-resident epilogues)
   int small_n;                 // recursion nodes of <= small_n tiles use the 64 x 32 pair-unit GEMM
                                // (GPRX_SMALL_N, default 8); larger ones the 64 x 64 core
   int diag_variant;            // 0: 4-wave k_diag, 1: one-wave k_diag_w (env GPRX_DIAGV)
   int xs;                      // row stride of Xc: 16 ceil(d/16) + 1 (odd: spreads LDS banks)
   int pst;                     // stride of params per slot
   int gps;                     // stride of per-unit gradient partials (d + 2)
-  int ngu;                     // gradient partial units per slot
+  int ngu;                     // gradient partial units per slot (lauum 2 x 2-tile units)
+  int nlj;                     // lauum jobs per slot (units folded in pairs)
   size_t ld, mat;              // ld = Npad, mat = Npad*Npad
   double* X;                   // B x [Npad][d]   (column t = one CState, contiguous d values)
   double* Xc;                  // B x [Npad][xs]  X minus its per-dimension mean over the N points,
@@ -57,7 +56,7 @@ struct DevBatch {
   double* out_var;             // B x Mpad
   int* status;                 // B
   int* info;                   // B
-  int* lauum_order;            // ngu x 2 (first row, column) of the lauum units, longest first
+  int* lauum_order;            // nlj x 6: two (first row, first column, unit id) per job, long + short
 };
 
 // GEMM operations of the recursive factorisation / inverse / prediction (tile units, see
@@ -97,6 +96,7 @@ void launch_gemm(const DevBatch& b, const GemmGeom& g, hipStream_t s, const Gemm
 void launch_alpha(const DevBatch& b, hipStream_t s, int phase);
 void launch_lauum_grad(const DevBatch& b, hipStream_t s);
 int lauum_units(int nt);
+int lauum_jobs(int nt);
 void lauum_order_host(int nt, int* out);
 void launch_finalize(const DevBatch& b, int want_grad, hipStream_t s);
 void launch_pred_cross(const DevBatch& b, hipStream_t s);

@@ -1251,7 +1251,18 @@ constexpr int SPW = DMAX + 2;  // per-wave partial row: S_p (d), S_f, T
 // (pr + wr, pc + wc) if on or below the diagonal.  LDS: the unit's four point tiles (raw [64][xs]
 // images, LDS-DMA before the MFMA loop), per-wave partials, the points' weighted norms, alpha and
 // il2.
+__device__ __forceinline__ void lauum_unit(const DevBatch& db, int slot, int pr, int pc, int u);
 __device__ __forceinline__ void lauum_body(const DevBatch& db) {
+  int slot, job;
+  if (!map_block(blockIdx.x, db.B, db.nlj, slot, job)) return;
+  const int* jb = db.lauum_order + 6 * job;
+  lauum_unit(db, slot, jb[0], jb[1], jb[2]);
+  if (jb[3] >= 0) {  // block-uniform: the folded short unit
+    __syncthreads();  // the first unit's LDS images and partials are consumed
+    lauum_unit(db, slot, jb[3], jb[4], jb[5]);
+  }
+}
+__device__ __forceinline__ void lauum_unit(const DevBatch& db, int slot, int pr, int pc, int u) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int d = db.d, tid = threadIdx.x, w = tid >> 6, wr = w >> 1, wc = w & 1;
   const int xs = db.xs, xt = TS * xs;  // point-tile image: [64][xs], dims >= d zero
@@ -1262,11 +1273,6 @@ __device__ __forceinline__ void lauum_body(const DevBatch& db) {
   double* als = nrm + 4 * TS;           // [4][64] alpha of the same points
   double* wl = als + 4 * TS;            // [DMAX] il2
   const int nt = db.nt;
-  int slot, u;
-  if (!map_block(blockIdx.x, db.B, db.ngu, slot, u)) return;
-  const int pr = db.lauum_order[2 * u], pc = db.lauum_order[2 * u + 1];  // longest K range first
-  if (db.delay > 0 && (blockIdx.x >> 8) == 1)  // blocks 256..511: the second resident WG per CU
-    for (int i = 0; i < db.delay; ++i) __builtin_amdgcn_s_sleep(127);
   const double* X = db.Xc + (size_t)slot * db.Npad * xs;
   const double* al = db.alpha + (size_t)slot * db.Npad;
   dma_tile(xr_s, X + (size_t)pr * xt, xt);
@@ -1435,16 +1441,28 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
   lauum_body(db);
 }
 int lauum_units(int nt) { return quad_units(nt, nt, true); }
+static bool lauum_fold() {
+  const char* e = getenv("GPRX_LAUUM_FOLD");  // experiment: 0 = one unit per workgroup
+  return !e || atoi(e) != 0;
+}
+int lauum_jobs(int nt) { return lauum_fold() ? (lauum_units(nt) + 1) / 2 : lauum_units(nt); }
 void lauum_order_host(int nt, int* out) {
-  // (first row, first column) of every 2 x 2-tile unit of the lower triangle, by row pair: the
-  // K range [row, nt) shrinks down the list (longest first)
-  int k = 0;
+  // 2 x 2-tile units of the lower triangle (first row, first column, unit id), K range [row, nt);
+  // folded into jobs of two: the i-th longest with the i-th shortest (then the middle one alone),
+  // jobs in decreasing order of their long unit.  6 ints per job; pr = -1 marks no second unit.
+  std::vector<int> us;
   for (int rp = 0; 2 * rp < nt; ++rp)
-    for (int cp = 0; cp <= rp; ++cp) {
-      out[2 * k] = 2 * rp;
-      out[2 * k + 1] = 2 * cp;
-      ++k;
-    }
+    for (int cp = 0; cp <= rp; ++cp) us.push_back(2 * rp), us.push_back(2 * cp);
+  const int n = (int)us.size() / 2, nj = lauum_jobs(nt);
+  for (int j = 0; j < nj; ++j) {
+    const int a = j, b = nj == n ? j : n - 1 - j;  // units are already in decreasing K order
+    out[6 * j + 0] = us[2 * a];
+    out[6 * j + 1] = us[2 * a + 1];
+    out[6 * j + 2] = a;
+    out[6 * j + 3] = (b != a) ? us[2 * b] : -1;
+    out[6 * j + 4] = (b != a) ? us[2 * b + 1] : -1;
+    out[6 * j + 5] = (b != a) ? b : -1;
+  }
 }
 
 // ============================================================================================
@@ -1644,7 +1662,7 @@ void launch_alpha(const DevBatch& b, hipStream_t s, int phase) {
 }
 void launch_lauum_grad(const DevBatch& b, hipStream_t s) {
   set_lds_limits();
-  hipLaunchKernelGGL(k_lauum_grad, dim3(grid_blocks(b.B, lauum_units(b.nt))), dim3(NTHR), lauum_lds(b.d), s, b);
+  hipLaunchKernelGGL(k_lauum_grad, dim3(grid_blocks(b.B, b.nlj)), dim3(NTHR), lauum_lds(b.d), s, b);
 }
 void launch_finalize(const DevBatch& b, int want_grad, hipStream_t s) {
   hipLaunchKernelGGL(k_finalize, dim3(b.B), dim3(NTHR), 0, s, b, want_grad);
