@@ -28,7 +28,8 @@ sys.path.insert(0, str(REPO / "gpr.jl_amd"))
 
 MECH, N, M, KEY = "P2", 2048, 100, 2048
 G = 6
-PEAK_FP64_TFLOPS = 78.6  # MI355X fp64 matrix (measured 77.6 with back-to-back v_mfma_f64_16x16x4)
+PEAK_FP64_TFLOPS = 78.6  # MI355X fp64 matrix peak (MI355X_MICROARCH.md); sustained under DVFS with random
+# operands: 61-67 TF/s measured (scratch/mfma_sustain.hip)
 PEAK_HBM_GBS = 8000.0
 
 
@@ -80,8 +81,10 @@ def pmc_traffic(stat: str, global_batch: int):
     return None
 
 
-def cpu_baseline(X, Y, T, XT, max_seconds: float = 15.0, max_fits: int = 32):
-    """Oracle (CPU restatement, numpy + OpenBLAS LAPACK) on a bounded sample of the same workload."""
+def cpu_baseline(X, Y, T, XT, gpu=None, max_seconds: float = 15.0, max_fits: int = 32):
+    """Oracle (CPU restatement, numpy + OpenBLAS LAPACK) on a bounded sample of the same workload.
+    With `gpu` (the last timed step's results) the same sample also gives the metric's accuracy
+    part: max |mu_gpu - mu_cpu| of the predictive means (BASELINE.json 'pred-mean max-err')."""
     sys.path.insert(0, str(REPO))
     from oracle import gp_oracle as O
 
@@ -93,16 +96,29 @@ def cpu_baseline(X, Y, T, XT, max_seconds: float = 15.0, max_fits: int = 32):
         threads = int(os.environ.get("OMP_NUM_THREADS", "1"))
     t0 = time.perf_counter()
     n = 0
+    err = dict(mu_abs=0.0, mu_rel=0.0, mll_rel=0.0, grad_rel=0.0)
     for s in range(min(max_fits, X.shape[0])):
-        O.fit(X[s], Y[s], T[s], XT[s])
+        f = O.fit(X[s], Y[s], T[s], XT[s])
         n += 1
+        if gpu is not None:
+            e_mu = float(np.max(np.abs(gpu["mu"][s] - f["mu"])))
+            err["mu_abs"] = max(err["mu_abs"], e_mu)
+            err["mu_rel"] = max(err["mu_rel"], e_mu / float(np.max(np.abs(Y[s]))))
+            err["mll_rel"] = max(err["mll_rel"], abs(gpu["mll"][s] - f["mll"]) / max(1.0, abs(f["mll"])))
+            err["grad_rel"] = max(err["grad_rel"], float(np.max(np.abs(gpu["grad"][s] - f["grad"])))
+                                  / max(1.0, float(np.max(np.abs(f["grad"])))))
         if time.perf_counter() - t0 > max_seconds:
             break
     dt = time.perf_counter() - t0
-    return dict(value=n / dt, unit="fits/s", cores=int(threads), kind="port",
+    base = dict(value=n / dt, unit="fits/s", cores=int(threads), kind="port",
                 sample=f"{n} P2 fits (N=2048, d=26, M=100) via oracle/gp_oracle.py: reference algorithm "
                        f"(Distances-style dist stack, OpenBLAS dpotrf, K^-1 by cho_solve(I), per-param grad "
                        f"sums), {dt:.1f}s, OpenBLAS threads={threads}")
+    acc = None
+    if gpu is not None:
+        acc = dict(err, slots=n, tolerance_mu_rel=1e-9, tolerance_mll_rel=1e-9, tolerance_grad_rel=1e-7,
+                   note="GPU vs CPU restatement on the same inputs; mu_rel = max|dmu| / max|y|")
+    return base, acc
 
 
 def main():
@@ -211,9 +227,9 @@ def main():
         opt = {"value": round(B * world / t_opt, 3), "unit": "optimised GP fits/s", "max_evals_per_gp": args.opt_evals,
                "device_rounds": rounds, "seconds": round(t_opt, 3),
                "stopped_by": {k: sum(1 for r in res if r.stopped_by == k) for k in sorted({r.stopped_by for r in res})}}
-    cpu = None
+    cpu = acc = None
     if rank == 0 and not args.no_cpu:
-        cpu = cpu_baseline(X, Y, T, XT)
+        cpu, acc = cpu_baseline(X, Y, T, XT, gpu=r)
 
     if rank == 0:
         out = {
@@ -238,6 +254,7 @@ def main():
             "roofline": roof,
             "kernels_ms_per_step": {k: round(v["ms"] / max(1, (min(args.steps, 3))), 3) for k, v in kern.items()} if kern else None,
             "cpu_baseline": cpu,
+            "pred_mean_max_err": acc,
             "optimise": opt,
         }
         print(json.dumps(out), flush=True)

@@ -300,7 +300,7 @@ void eval_group(gprx_ctx* c, hipStream_t st, const DevBatch& db, bool want_grad,
   timed(c, st, "alpha", Bd * Np * Np, Bd * 8.0 * Np * Np / 2.0, [&] { gprx::launch_alpha(db, st, 1); });
   if (want_grad)
     timed(c, st, "lauum_grad", Bd * (Np * Np * Np / 3.0 + 2.0 * Np * Np * d + 4.0 * Np * Np),
-          Bd * 8.0 * (Np * Np / 2.0 + TS * TS * (nt * (nt + 1.0) * (nt + 2.0) / 3.0)),
+          Bd * 8.0 * (Np * Np / 2.0 + Np * (db.xs + 2.0)),  // minimum: Mt upper, Xc, alpha once
           [&] { gprx::launch_lauum_grad(db, st); });
   timed(c, st, "finalize", Bd * 2.0 * db.N, Bd * 16.0 * db.N, [&] { gprx::launch_finalize(db, want_grad ? 1 : 0, st); });
   if (want_pred) predict_group(c, st, db);
