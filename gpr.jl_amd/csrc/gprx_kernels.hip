@@ -1134,54 +1134,93 @@ __device__ __forceinline__ void acc_store_t(double* Ct, size_t ld, const d4 (&ac
       for (int q = 0; q < 4; ++q) Ct[(size_t)(16 * a + lr) * ld + 16 * b + lk + 4 * q] = sgn * acc[a][b][q];
 }
 
+// 64 x 64 accumulator tile stores (C layout of mma_64x64): C[r + c ld] = sgn acc, and the
+// transposed Ct[c + r ld] = sgn acc through a per-wave [16][65] LDS buffer (contiguous 512-B
+// column segments instead of 16-way scattered rows).
+__device__ __forceinline__ void acc4_store(double* C, size_t ld, const d4 (&acc)[QM][QN], double sgn) {
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+#pragma unroll
+  for (int a = 0; a < QM; ++a)
+#pragma unroll
+    for (int b = 0; b < QN; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) C[(size_t)(16 * b + lk + 4 * q) * ld + 16 * a + lr] = sgn * acc[a][b][q];
+}
+__device__ __forceinline__ void acc4_store_t(double* Ct, size_t ld, const d4 (&acc)[QM][QN], double sgn, double* tb) {
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+#pragma unroll
+  for (int a = 0; a < QM; ++a) {
+#pragma unroll
+    for (int b = 0; b < QN; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) tb[lr * (TS + 1) + 16 * b + lk + 4 * q] = sgn * acc[a][b][q];
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) Ct[(size_t)(16 * a + r) * ld + l] = tb[r * (TS + 1) + l];
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 __device__ __forceinline__ void leaf_body(const DevBatch& db, int o, int n) {
+  // one 64 x 64 tile task per wave (4 at a time); tile stores through the wave's LDS buffer
+  __shared__ double tbs[4 * 16 * (TS + 1)];
   const int slot = blockIdx.x;
-  const int w = threadIdx.x >> 6, half = w & 1, tw = w >> 1;
+  const int w = threadIdx.x >> 6;
+  double* tb = tbs + w * 16 * (TS + 1);
   const size_t ld = db.ld, so = (size_t)slot * db.mat;
   double* K = db.K + so;
   double* Lw = db.Lw + so;
   double* Li = db.Linv + so;
   double* Mt = db.Mt + so;
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
   for (int k = 0; k < n; ++k) {
     const int tk = o + k, m = n - 1 - k;
     if (!(db.ablate & 8)) diag_tile_fast(db, slot, tk);  // ablate bits: timing experiments only
     __syncthreads();
-    for (int t = tw; t < ((db.ablate & 16) ? 0 : m); t += 2) {  // TRSM
+    for (int t = w; t < ((db.ablate & 16) ? 0 : m); t += 4) {  // TRSM: L[ti,tk] = K[ti,tk] Linv[tk,tk]^T
       const int ti = tk + 1 + t;
-      d4 acc[WM][WN];
-      acc_zero(acc);
-      mma_64x32(acc, K + (size_t)tk * TS * ld + ti * TS, ld, Li + (size_t)tk * TS * ld + tk * TS + 32 * half, ld, TS);
-      acc_store(Lw + (size_t)(tk * TS + 32 * half) * ld + ti * TS, ld, acc, 1.0);
+      d4 acc[QM][QN];
+      acc4_zero(acc);
+      mma_64x64(acc, K + (size_t)tk * TS * ld + ti * TS, ld, Li + (size_t)tk * TS * ld + tk * TS, ld, TS);
+      acc4_store(Lw + (size_t)(tk * TS) * ld + ti * TS, ld, acc, 1.0);
     }
     __syncthreads();
-    for (int t = tw; t < ((db.ablate & 16) ? 0 : m * (m + 1) / 2); t += 2) {  // SYRK (lower tiles of the trailing block)
+    for (int t = w; t < ((db.ablate & 16) ? 0 : m * (m + 1) / 2); t += 4) {  // SYRK (lower trailing tiles)
       int a = t, c = 0;
       while (a >= m - c) {
         a -= m - c;
         ++c;
       }
       const int tj = tk + 1 + c, ti = tj + a;
-      d4 acc[WM][WN];
-      acc_zero(acc);
-      mma_64x32(acc, Lw + (size_t)tk * TS * ld + ti * TS, ld, Lw + (size_t)tk * TS * ld + tj * TS + 32 * half, ld, TS);
-      acc_sub(K + (size_t)(tj * TS + 32 * half) * ld + ti * TS, ld, acc);
+      double* Ct = K + (size_t)(tj * TS) * ld + ti * TS;
+      d4 acc[QM][QN];  // -C - L L^T, stored negated
+#pragma unroll
+      for (int aa = 0; aa < QM; ++aa)
+#pragma unroll
+        for (int b = 0; b < QN; ++b)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc[aa][b][q] = -Ct[(size_t)(16 * b + lk + 4 * q) * ld + 16 * aa + lr];
+      mma_64x64(acc, Lw + (size_t)tk * TS * ld + ti * TS, ld, Lw + (size_t)tk * TS * ld + tj * TS, ld, TS);
+      acc4_store(Ct, ld, acc, -1.0);
     }
     __syncthreads();
   }
+  // off-diagonal inverse tiles by sub-diagonal s:  X = sum_{k=tj}^{ti-1} L[ti,k] Linv[k,tj] (kept
+  // transposed in Mt[tj,ti] as scratch), Linv[ti,tj] = -Linv[ti,ti] X; one wave per tile
   for (int s = 1; s < ((db.ablate & 32) ? 0 : n); ++s) {
-    for (int t = tw; t < n - s; t += 2) {
+    for (int t = w; t < n - s; t += 4) {
       const int tj = o + t, ti = tj + s;
-      double* Xt = Mt + (size_t)(ti * TS) * ld + tj * TS + 32 * half;  // Mt[tj,ti], this wave's rows
-      d4 acc[WM][WN];
-      acc_zero(acc);
-      mma_64x32(acc, Lw + (size_t)tj * TS * ld + ti * TS, ld, Mt + (size_t)tj * TS * ld + tj * TS + 32 * half, ld, s * TS);
-      acc_store_t(Xt, ld, acc, 1.0);
+      double* Xt = Mt + (size_t)(ti * TS) * ld + tj * TS;  // Mt[tj,ti]
+      d4 acc[QM][QN];
+      acc4_zero(acc);
+      mma_64x64(acc, Lw + (size_t)tj * TS * ld + ti * TS, ld, Mt + (size_t)tj * TS * ld + tj * TS, ld, s * TS);
+      acc4_store_t(Xt, ld, acc, 1.0, tb);
       __threadfence_block();
-      acc_zero(acc);
-      mma_64x32(acc, Li + (size_t)ti * TS * ld + ti * TS, ld, Xt, ld, TS);
+      acc4_zero(acc);
+      mma_64x64(acc, Li + (size_t)ti * TS * ld + ti * TS, ld, Xt, ld, TS);
       __threadfence_block();  // all lanes' reads of X precede the overwrite below
-      acc_store(Li + (size_t)(tj * TS + 32 * half) * ld + ti * TS, ld, acc, -1.0);
-      acc_store_t(Xt, ld, acc, -1.0);
+      acc4_store(Li + (size_t)(tj * TS) * ld + ti * TS, ld, acc, -1.0);
+      acc4_store_t(Xt, ld, acc, -1.0, tb);
     }
     __syncthreads();
   }
