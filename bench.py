@@ -191,7 +191,7 @@ def main():
             batch.run(T, grad=True, predict=True)
         ctx.set_profiling(False)
         names = ["gram", "leaf", "diag", "potrf_trsm", "potrf_syrk", "trtri_tt", "syrk_tt", "trtri_linv21", "alpha", "lauum_grad",
-                 "finalize", "pred_cross", "pred_var", "pred_final"]
+                 "finalize", "pred_cross", "pred_var", "pred_mu", "pred_final"]
         for nme in names:
             kern[nme] = ctx.kernel_stats(nme)
         dom = max(kern, key=lambda k: kern[k]["ms"])

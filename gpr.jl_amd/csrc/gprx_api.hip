@@ -54,6 +54,10 @@ struct gprx_ctx {
   int stagger = -1;                   // GPRX_STAGGER: -1 groups start together; 0 / 1 group g starts
                                       // after group g-1's Gram / factorisation
   std::vector<hipEvent_t> smarks;     // stagger events (nstreams)
+  std::vector<hipStream_t> sstreams;  // prediction side stream per group
+  std::vector<hipEvent_t> sevents;    // 3 per group: fork, factorised, join
+  bool side = false;                  // GPRX_SIDE=1: prediction on a side stream (measured no gain:
+                                      // the big kernels fill the register file, nothing co-resides)
 };
 
 struct gprx_batch {
@@ -276,26 +280,52 @@ void factor_rec(gprx_ctx* c, hipStream_t st, const DevBatch& db, int o, int n) {
   timed(c, st, "trtri_linv21", f_linv, b_linv, [&] { gprx::launch_gemm(db, g, st); }, n);
 }
 
-void predict_group(gprx_ctx* c, hipStream_t st, const DevBatch& db) {
+void predict_cross(gprx_ctx* c, hipStream_t st, const DevBatch& db) {
   const double N = db.N, M = db.M, d = db.d, B = db.B;
-  timed(c, st, "pred_cross", B * (3.0 * N * M * d + 2.0 * N * M), B * 8.0 * (N * db.Mpad + (N + M) * d),
+  timed(c, st, "pred_cross", B * 3.0 * N * M * d, B * 8.0 * (N * db.Mpad + (N + M) * d),
         [&] { gprx::launch_pred_cross(db, st); });
+}
+void predict_var(gprx_ctx* c, hipStream_t st, const DevBatch& db) {
+  const double N = db.N, M = db.M, B = db.B;
   gprx::GemmGeom g{gprx::OP_PREDVAR, 0, 0, 0};
   timed(c, st, "pred_var", B * N * N * M, B * 8.0 * (N * N / 2 + N * db.Mpad), [&] { gprx::launch_gemm(db, g, st); });
+}
+void predict_mean_final(gprx_ctx* c, hipStream_t st, const DevBatch& db) {
+  const double N = db.N, M = db.M, B = db.B;
+  timed(c, st, "pred_mu", B * 2.0 * N * M, B * 8.0 * (N * db.Mpad + N), [&] { gprx::launch_pred_mu(db, st); });
   timed(c, st, "pred_final", B * 2.0 * db.nt * db.Mpad, B * 16.0 * db.nt * db.Mpad,
         [&] { gprx::launch_pred_final(db, st); });
 }
+void predict_group(gprx_ctx* c, hipStream_t st, const DevBatch& db) {
+  predict_cross(c, st, db);
+  predict_var(c, st, db);
+  predict_mean_final(c, st, db);
+}
 
-// Whole evaluation of one slot group on one stream.  `mark` (optional) is recorded once the
-// group's factorisation is queued (the stagger point of concurrent slot groups).
+// Whole evaluation of one slot group on stream `st`, with the prediction's K*^T and variance GEMM
+// on the side stream `ss` (they need only the factorisation, so they run beside alpha and the
+// gradient).  `mark` (optional) is recorded once the group's factorisation is queued (the
+// stagger point of concurrent slot groups); ev[0..2] are the fork / factorised / join events.
 void eval_group(gprx_ctx* c, hipStream_t st, const DevBatch& db, bool want_grad, bool want_pred,
-                hipEvent_t mark = nullptr) {
+                hipEvent_t mark = nullptr, hipStream_t ss = nullptr, hipEvent_t* ev = nullptr) {
   const double Bd = db.B, nt = db.nt, Np = db.Npad, d = db.d;
+  const bool side = want_pred && ss && ev;
+  if (side) {
+    (void)hipEventRecord(ev[0], st);
+    (void)hipStreamWaitEvent(ss, ev[0], 0);
+    predict_cross(c, ss, db);
+  }
   timed(c, st, "gram", Bd * 3.0 * db.N * (double)db.N * d / 2.0, Bd * 8.0 * (Np * Np / 2.0 + Np * d),
         [&] { gprx::launch_gram(db, st); });
   if (mark && c->stagger == 0) (void)hipEventRecord(mark, st);
   factor_rec(c, st, db, 0, db.nt);
   if (mark && c->stagger == 1) (void)hipEventRecord(mark, st);
+  if (side) {
+    (void)hipEventRecord(ev[1], st);
+    (void)hipStreamWaitEvent(ss, ev[1], 0);
+    predict_var(c, ss, db);
+    (void)hipEventRecord(ev[2], ss);
+  }
   timed(c, st, "alpha", Bd * Np * Np, Bd * 8.0 * Np * Np / 2.0, [&] { gprx::launch_alpha(db, st, 0); });
   timed(c, st, "alpha", Bd * Np * Np, Bd * 8.0 * Np * Np / 2.0, [&] { gprx::launch_alpha(db, st, 1); });
   if (want_grad)
@@ -303,7 +333,12 @@ void eval_group(gprx_ctx* c, hipStream_t st, const DevBatch& db, bool want_grad,
           Bd * 8.0 * (Np * Np / 2.0 + Np * (db.xs + 2.0)),  // minimum: Mt upper, Xc, alpha once
           [&] { gprx::launch_lauum_grad(db, st); });
   timed(c, st, "finalize", Bd * 2.0 * db.N, Bd * 16.0 * db.N, [&] { gprx::launch_finalize(db, want_grad ? 1 : 0, st); });
-  if (want_pred) predict_group(c, st, db);
+  if (side) {
+    (void)hipStreamWaitEvent(st, ev[2], 0);
+    predict_mean_final(c, st, db);
+  } else if (want_pred) {
+    predict_group(c, st, db);
+  }
 }
 
 // Fork the slot groups of `b` over the context's group streams, join back on the main stream.
@@ -321,7 +356,8 @@ int run_graph(gprx_batch* b, bool want_grad, bool want_pred) {
     b->gvalid[gi] = false;
     hipGraph_t graph = nullptr;
     HIPCHK(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-    eval_group(c, c->stream, db, want_grad, want_pred);
+    eval_group(c, c->stream, db, want_grad, want_pred, nullptr, c->side ? c->sstreams[0] : nullptr,
+               c->side ? &c->sevents[0] : nullptr);
     const hipError_t le = hipGetLastError();
     const hipError_t ce = hipStreamEndCapture(c->stream, &graph);
     if (le != hipSuccess || ce != hipSuccess) {
@@ -353,7 +389,9 @@ int run_groups(gprx_batch* b, bool want_grad, bool want_pred, bool factor) {
     // staggered groups: group g starts when group g-1 has passed its stagger point
     if (g > 0 && c->stagger >= 0 && factor) HIPCHK(c, hipStreamWaitEvent(st, c->smarks[g - 1], 0));
     const DevBatch v = sub_batch(db, s0, cnt);
-    if (factor) eval_group(c, st, v, want_grad, want_pred, c->stagger >= 0 ? c->smarks[g] : nullptr);
+    if (factor)
+      eval_group(c, st, v, want_grad, want_pred, c->stagger >= 0 ? c->smarks[g] : nullptr,
+                 c->side ? c->sstreams[g] : nullptr, c->side ? &c->sevents[3 * g] : nullptr);
     else if (want_pred) predict_group(c, st, v);
     HIPCHK(c, hipEventRecord(c->gevents[1 + g], st));
     HIPCHK(c, hipStreamWaitEvent(c->stream, c->gevents[1 + g], 0));
@@ -401,6 +439,13 @@ int gprx_ctx_create(int device, gprx_ctx** out) {
   c->gstreams.resize(c->nstreams);
   c->gevents.resize(1 + c->nstreams);
   c->smarks.resize(c->nstreams);
+  if (const char* sd = getenv("GPRX_SIDE")) c->side = atoi(sd) != 0;
+  c->sstreams.resize(c->nstreams);
+  c->sevents.resize(3 * c->nstreams);
+  for (auto& st : c->sstreams)
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return GPRX_DEVICE_ERROR;
+  for (auto& e : c->sevents)
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return GPRX_DEVICE_ERROR;
   for (auto& e : c->smarks)
     if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return GPRX_DEVICE_ERROR;
   for (auto& st : c->gstreams)
@@ -426,6 +471,11 @@ void gprx_ctx_destroy(gprx_ctx* c) {
   }
   for (auto e : c->gevents) (void)hipEventDestroy(e);
   for (auto e : c->smarks) (void)hipEventDestroy(e);
+  for (auto st : c->sstreams) {
+    (void)hipStreamSynchronize(st);
+    (void)hipStreamDestroy(st);
+  }
+  for (auto e : c->sevents) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(c->stream);
   delete c;
 }

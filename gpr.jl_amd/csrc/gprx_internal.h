@@ -100,6 +100,7 @@ int lauum_jobs(int nt);
 void lauum_order_host(int nt, int* out);
 void launch_finalize(const DevBatch& b, int want_grad, hipStream_t s);
 void launch_pred_cross(const DevBatch& b, hipStream_t s);
+void launch_pred_mu(const DevBatch& b, hipStream_t s);
 void launch_pred_final(const DevBatch& b, hipStream_t s);
 
 }  // namespace gprx

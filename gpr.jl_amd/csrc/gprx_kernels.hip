@@ -301,6 +301,7 @@ __device__ __forceinline__ void acc_zero(d4 (&acc)[WM][WN]) {
 // Gram: lower tiles of K (noise on the diagonal).  grid = B * ntl, 256 threads, each thread
 // a 4x4 register block; X tiles in dynamic LDS as [p][64].
 // ============================================================================================
+template <int MODE>
 __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int d = db.d, tid = threadIdx.x;
@@ -328,7 +329,7 @@ __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
   for (int e = tid; e < d + 3; e += NTHR) pw[e] = P[e];
   __syncthreads();
   const double sf2 = pw[d], noise = pw[d + 1];
-  const int rb = tid & 15, cb = tid >> 4, mode = db.dist_mode;
+  const int rb = tid & 15, cb = tid >> 4;
   double rr[4][4];
 #pragma unroll
   for (int a = 0; a < 4; ++a)
@@ -351,7 +352,7 @@ __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
-      for (int b = 0; b < 4; ++b) rr[a][b] = rr[a][b] + sqd2(av[a], a2[a], bv[b], b2[b], mode) * w;
+      for (int b = 0; b < 4; ++b) rr[a][b] = rr[a][b] + sqd2(av[a], a2[a], bv[b], b2[b], MODE) * w;
   }
   double* K = db.K + (size_t)slot * db.mat;
 #pragma unroll
@@ -965,7 +966,7 @@ __device__ __forceinline__ void gemm_body(const DevBatch& db, const GemmGeom& g1
       pc2 = UC * f;
       np = (CU - 1 - f != f) ? 2 : 1;
     } else {  // fold rows; TT: K shrinks with the row, LINV21 / PREDVAR: K grows with the row
-      const int nf = (RU + 1) / 2, f = u / CU, pj = u - f * CU;
+      const int f = u / CU, pj = u - f * CU;
       const int lo = f, hi = RU - 1 - f;
       pr = UR * (op == OP_TT ? lo : hi);
       pr2 = UR * (op == OP_TT ? hi : lo);
@@ -1556,18 +1557,16 @@ __global__ __launch_bounds__(NTHR) void k_finalize(DevBatch db, int want_grad) {
 //   (pred_var : OP_PREDVAR of k_gemm, V = Linv K*, column sums of V^2)
 //   pred_final: mu = sum mu_part, var = max(sf2 - sum var_part, 0).       grid = B
 // ============================================================================================
+template <int MODE>
 __global__ __launch_bounds__(NTHR) void k_pred_cross(DevBatch db) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int d = db.d, tid = threadIdx.x;
   double* xt = sm;
   double* xs = sm + d * TS;
   double* pw = sm + 2 * d * TS;
-  double* at = pw + DMAX + 4;
-  double* part = at + TS;  // [16][64]
   int slot, t;
   if (!map_block(blockIdx.x, db.B, db.nt * db.mt, slot, t)) return;
   const int ch = t / db.mt, mtile = t - ch * db.mt;
-  const int mode = db.dist_mode;
   const double* X = db.X + (size_t)slot * db.Npad * d;
   const double* Xq = db.Xs + (size_t)slot * db.Mpad * d;
   for (int e = tid; e < TS * d; e += NTHR) {
@@ -1577,7 +1576,6 @@ __global__ __launch_bounds__(NTHR) void k_pred_cross(DevBatch db) {
   }
   const double* P = db.params + (size_t)slot * db.pst;
   for (int e = tid; e < d + 3; e += NTHR) pw[e] = P[e];
-  if (tid < TS) at[tid] = db.alpha[(size_t)slot * db.Npad + ch * TS + tid];
   __syncthreads();
   const double sf2 = pw[d];
   // thread: 4 test points (4mb..) x 4 train points (4rb..)
@@ -1604,10 +1602,9 @@ __global__ __launch_bounds__(NTHR) void k_pred_cross(DevBatch db) {
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
-      for (int b = 0; b < 4; ++b) rr[a][b] = rr[a][b] + sqd2(av[a], a2[a], bv[b], b2[b], mode) * wgt;
+      for (int b = 0; b < 4; ++b) rr[a][b] = rr[a][b] + sqd2(av[a], a2[a], bv[b], b2[b], MODE) * wgt;
   }
   double* KsT = db.KsT + (size_t)slot * db.Npad * db.Mpad;
-  double macc[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
   for (int a = 0; a < 4; ++a) {  // train point gt
     const int gt = ch * TS + 4 * rb + a;
@@ -1616,19 +1613,32 @@ __global__ __launch_bounds__(NTHR) void k_pred_cross(DevBatch db) {
     for (int b = 0; b < 4; ++b) {
       const int gm = mtile * TS + 4 * mb + b;
       kv[b] = (gt < db.N && gm < db.M) ? sf2 * exp(-rr[a][b] * 0.5) : 0.0;
-      macc[b] = fma(kv[b], at[4 * rb + a], macc[b]);
     }
     double* o = KsT + (size_t)gt * db.Mpad + mtile * TS + 4 * mb;
     *(double2*)o = make_double2(kv[0], kv[1]);
     *(double2*)(o + 2) = make_double2(kv[2], kv[3]);
   }
-#pragma unroll
-  for (int b = 0; b < 4; ++b) part[rb * TS + 4 * mb + b] = macc[b];
-  __syncthreads();
-  if (tid < TS) {
+}
+
+// Partial predictive means per training tile: mu_part[ch][m] = sum_{t in tile ch} K*^T[t][m] alpha_t.
+// grid = B * nt.  (Separate from k_pred_cross so that K*^T and the variance GEMM need only the
+// factorisation and can run beside alpha / the gradient on a second stream.)
+__global__ __launch_bounds__(NTHR) void k_pred_mu(DevBatch db) {
+  __shared__ double part[2][NTHR];
+  int slot, ch;
+  if (!map_block(blockIdx.x, db.B, db.nt, slot, ch)) return;
+  const double* KsT = db.KsT + ((size_t)slot * db.Npad + (size_t)ch * TS) * db.Mpad;
+  const double* al = db.alpha + (size_t)slot * db.Npad + ch * TS;
+  const int tid = threadIdx.x, h = tid >> 7, mm = tid & 127;
+  for (int m0 = 0; m0 < db.Mpad; m0 += 128) {
+    const int m = m0 + mm;
     double s = 0.0;
-    for (int k = 0; k < 16; ++k) s += part[k * TS + tid];
-    db.mu_part[((size_t)slot * db.nt + ch) * db.Mpad + mtile * TS + tid] = s;
+    if (m < db.Mpad)
+      for (int t = 32 * h; t < 32 * h + 32; ++t) s = fma(KsT[(size_t)t * db.Mpad + m], al[t], s);
+    part[0][tid] = s;
+    __syncthreads();
+    if (h == 0 && m < db.Mpad) db.mu_part[((size_t)slot * db.nt + ch) * db.Mpad + m] = part[0][mm] + part[0][128 + mm];
+    __syncthreads();
   }
 }
 
@@ -1654,20 +1664,23 @@ static size_t gram_lds(int d) { return (size_t)(2 * d * TS + DMAX + 4) * sizeof(
 static size_t lauum_lds(int d) {
   return (size_t)(4 * (16 * ((d + 15) / 16) + 1) * TS + 4 * SPW + 8 * TS + DMAX) * sizeof(double);
 }
-static size_t cross_lds(int d) { return (size_t)(2 * d * TS + DMAX + 4 + TS + 16 * TS) * sizeof(double); }
+static size_t cross_lds(int d) { return (size_t)(2 * d * TS + DMAX + 4) * sizeof(double); }
 
 static void set_lds_limits() {
   static bool done = false;
   if (done) return;
   done = true;
-  (void)hipFuncSetAttribute((const void*)k_gram, hipFuncAttributeMaxDynamicSharedMemorySize, (int)gram_lds(DMAX));
+  for (const void* f : {(const void*)k_gram<0>, (const void*)k_gram<1>})
+    (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)gram_lds(DMAX));
   (void)hipFuncSetAttribute((const void*)k_lauum_grad, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lauum_lds(DMAX));
-  (void)hipFuncSetAttribute((const void*)k_pred_cross, hipFuncAttributeMaxDynamicSharedMemorySize, (int)cross_lds(DMAX));
+  for (const void* f : {(const void*)k_pred_cross<0>, (const void*)k_pred_cross<1>})
+    (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)cross_lds(DMAX));
 }
 
 void launch_gram(const DevBatch& b, hipStream_t s) {
   set_lds_limits();
-  hipLaunchKernelGGL(k_gram, dim3(grid_blocks(b.B, b.ntl)), dim3(NTHR), gram_lds(b.d), s, b);
+  if (b.dist_mode == 0) hipLaunchKernelGGL(k_gram<0>, dim3(grid_blocks(b.B, b.ntl)), dim3(NTHR), gram_lds(b.d), s, b);
+  else hipLaunchKernelGGL(k_gram<1>, dim3(grid_blocks(b.B, b.ntl)), dim3(NTHR), gram_lds(b.d), s, b);
 }
 void launch_center(const DevBatch& b, hipStream_t s) { hipLaunchKernelGGL(k_center, dim3(b.B), dim3(NTHR), 0, s, b); }
 void launch_diag(const DevBatch& b, int jt, hipStream_t s) {
@@ -1708,7 +1721,12 @@ void launch_finalize(const DevBatch& b, int want_grad, hipStream_t s) {
 }
 void launch_pred_cross(const DevBatch& b, hipStream_t s) {
   set_lds_limits();
-  hipLaunchKernelGGL(k_pred_cross, dim3(grid_blocks(b.B, b.nt * b.mt)), dim3(NTHR), cross_lds(b.d), s, b);
+  const dim3 grid(grid_blocks(b.B, b.nt * b.mt));
+  if (b.dist_mode == 0) hipLaunchKernelGGL(k_pred_cross<0>, grid, dim3(NTHR), cross_lds(b.d), s, b);
+  else hipLaunchKernelGGL(k_pred_cross<1>, grid, dim3(NTHR), cross_lds(b.d), s, b);
+}
+void launch_pred_mu(const DevBatch& b, hipStream_t s) {
+  hipLaunchKernelGGL(k_pred_mu, dim3(grid_blocks(b.B, b.nt)), dim3(NTHR), 0, s, b);
 }
 void launch_pred_final(const DevBatch& b, hipStream_t s) {
   hipLaunchKernelGGL(k_pred_final, dim3(b.B), dim3(NTHR), 0, s, b);

@@ -16,7 +16,7 @@ for trials in [int(a) for a in sys.argv[1:]] or [1, 4, 8, 16]:
     ctx.set_profiling(True); ctx.reset_stats()
     b.run(T, grad=True, predict=True)
     ctx.set_profiling(False)
-    ks = {k: ctx.kernel_stats(k) for k in ["gram","leaf","diag","potrf_trsm","potrf_syrk","trtri_tt","syrk_tt","trtri_linv21","alpha","lauum_grad","finalize","pred_cross","pred_var","pred_final"]}
+    ks = {k: ctx.kernel_stats(k) for k in ["gram","leaf","diag","potrf_trsm","potrf_syrk","trtri_tt","syrk_tt","trtri_linv21","alpha","lauum_grad","finalize","pred_cross","pred_var","pred_mu","pred_final"]}
     tot = sum(v['ms'] for v in ks.values())
     print(f"trials={trials} B={B}: {dt*1e3:.2f} ms/step  {B/dt:.1f} fits/s  {B*bench.fit_flops(2048,26,100)/dt/1e12:.2f} TF  status_ok={bool((r['status']==0).all())}  prof_sum={tot:.2f}ms", flush=True)
     for k, v in ks.items():
