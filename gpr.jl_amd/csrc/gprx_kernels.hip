@@ -108,6 +108,27 @@ __device__ __forceinline__ void sqrt_rsqrt(double p, double& s, double& r) {
   s = p * r;
   s = fma(0.5 * r, fma(-s, s, p), s);
 }
+// exp(x) for x <= 0, relative error < 1e-14 (degree-11 Taylor on |r| <= ln2/2 after the
+// Cody-Waite reduction x = n ln2 + r): 17 instructions, no range checks beyond underflow.  Used
+// only for the gradient's recomputed Kf (tolerance 1e-7); K itself uses the library exp.
+__device__ __forceinline__ double exp_neg(double x) {
+  const double n = rint(x * 1.4426950408889634);
+  double r = fma(-n, 6.93147180369123816490e-01, x);
+  r = fma(-n, 1.90821492927058770002e-10, r);
+  double p = 2.505210838544172e-08;  // 1/11!
+  p = fma(p, r, 2.755731922398589e-07);
+  p = fma(p, r, 2.7557319223985893e-06);
+  p = fma(p, r, 2.48015873015873e-05);
+  p = fma(p, r, 1.984126984126984e-04);
+  p = fma(p, r, 1.388888888888889e-03);
+  p = fma(p, r, 8.333333333333333e-03);
+  p = fma(p, r, 4.1666666666666664e-02);
+  p = fma(p, r, 1.6666666666666666e-01);
+  p = fma(p, r, 0.5);
+  p = fma(p, r, 1.0);
+  p = fma(p, r, 1.0);
+  return x < -745.0 ? 0.0 : ldexp(p, (int)n);
+}
 // 1/p by v_rcp_f64 + two Newton steps (|error| <= 1 ulp; the reference's dpotf2 scales by 1/ajj too)
 __device__ __forceinline__ double recip(double p) {
   double r = __builtin_amdgcn_rcp(p);
@@ -1362,7 +1383,6 @@ __device__ __forceinline__ void lauum_unit(const DevBatch& db, int slot, int pr,
 #pragma unroll
       for (int b = 0; b < QN; ++b) {
         d4 cr = (d4){0.0, 0.0, 0.0, 0.0};
-#pragma unroll 4
         for (int s2 = 0; s2 < KS; ++s2) {
           const int k = 4 * s2 + lk;
           const double xa = wl[k < d ? k : 0] * xr[(16 * a + lr) * xs + k];  // xr = 0 for k >= d
@@ -1381,7 +1401,7 @@ __device__ __forceinline__ void lauum_unit(const DevBatch& db, int slot, int pr,
               tr += W;
             } else {
               const double rr = fma(-2.0, cr[q], nr[r] + nc[c]);
-              const double kf = (db.ablate & 64) ? 1.0 : sf2 * exp(-0.5 * (rr > 0.0 ? rr : 0.0));
+              const double kf = (db.ablate & 64) ? 1.0 : sf2 * exp_neg(-0.5 * (rr > 0.0 ? rr : 0.0));
               G = W * kf;
             }
             sf += G;
