@@ -137,6 +137,7 @@ DevBatch sub_batch(const DevBatch& db, int s0, int cnt) {
   v.Linv += s * db.mat;
   v.Mt += s * db.mat;
   v.z += s * db.Npad;
+  v.zp += s * 2 * db.nt * (size_t)db.Npad;
   v.alpha += s * db.Npad;
   v.params += s * db.pst;
   v.logdet_part += s * db.nt;
@@ -326,7 +327,7 @@ void eval_group(gprx_ctx* c, hipStream_t st, const DevBatch& db, bool want_grad,
     predict_var(c, ss, db);
     (void)hipEventRecord(ev[2], ss);
   }
-  timed(c, st, "alpha", Bd * Np * Np, Bd * 8.0 * Np * Np / 2.0, [&] { gprx::launch_alpha(db, st, 0); });
+  timed(c, st, "alpha", Bd * Np * nt, Bd * 8.0 * Np * nt, [&] { gprx::launch_alpha(db, st, 0); });
   timed(c, st, "alpha", Bd * Np * Np, Bd * 8.0 * Np * Np / 2.0, [&] { gprx::launch_alpha(db, st, 1); });
   if (want_grad)
     timed(c, st, "lauum_grad", Bd * (Np * Np * Np / 3.0 + 2.0 * Np * Np * d + 4.0 * Np * Np),
@@ -555,6 +556,7 @@ int gprx_batch_create(gprx_ctx* c, int B, int d, int N, int M_max, gprx_batch** 
   if ((rc = dalloc(b, &db.Linv, Bs * db.mat))) return fail(rc);
   if ((rc = dalloc(b, &db.Mt, Bs * db.mat))) return fail(rc);
   if ((rc = dalloc(b, &db.z, Bs * db.Npad))) return fail(rc);
+  if ((rc = dalloc(b, &db.zp, Bs * 2 * db.nt * (size_t)db.Npad))) return fail(rc);
   if ((rc = dalloc(b, &db.alpha, Bs * db.Npad))) return fail(rc);
   if ((rc = dalloc(b, &db.params, Bs * db.pst))) return fail(rc);
   if ((rc = dalloc(b, &db.logdet_part, Bs * db.nt))) return fail(rc);

@@ -42,6 +42,7 @@ struct DevBatch {
   double* Linv;                // B x mat
   double* Mt;                  // B x mat
   double* z;                   // B x Npad        z = L^{-1} y
+  double* zp;                  // B x 2nt x Npad  per-tile partials of z (see zp_acc4)
   double* alpha;               // B x Npad        alpha = K^{-1} y
   double* params;              // B x pst: [0,d) il2 = exp(-2 log ell), d: sf2, d+1: noise diag
                                //          (sn2 + eps), d+2: sn2

@@ -150,6 +150,39 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
+// per-tile partials of z = L^-1 y (see zp_acc4)
+__device__ __forceinline__ double* zp_row(const DevBatch& db, int slot, int h) {
+  return db.zp + ((size_t)slot * 2 * db.nt + h) * db.Npad;
+}
+// a diagonal tile from an LDS image: row r of X at img[r * rs + c * cs].  With a 256-thread
+// workgroup and a [256]-double scratch the 64 columns are split in 4 quarters (no serial chain);
+// call from every thread of the workgroup (contains barriers when scr != nullptr).
+__device__ __forceinline__ void zp_diag(const DevBatch& db, int slot, int jt, const double* img, int rs, int cs,
+                                        double* scr = nullptr) {
+  const double* y = db.Y + (size_t)slot * db.Npad + jt * TS;
+  if (scr) {
+    const int r = threadIdx.x & 63, qc = threadIdx.x >> 6;
+    double t = 0.0;
+#pragma unroll
+    for (int c = 16 * qc; c < 16 * qc + 16; ++c) t = fma(img[r * rs + c * cs], y[c], t);  // X upper = 0
+    __syncthreads();
+    scr[qc * TS + r] = t;
+    __syncthreads();
+    if (qc == 0) {
+      zp_row(db, slot, 2 * jt)[jt * TS + r] = ((scr[r] + scr[TS + r]) + scr[2 * TS + r]) + scr[3 * TS + r];
+      zp_row(db, slot, 2 * jt + 1)[jt * TS + r] = 0.0;
+    }
+    __syncthreads();
+    return;
+  }
+  const int r = threadIdx.x;
+  if (r >= TS) return;
+  double t = 0.0;
+  for (int c = 0; c <= r; ++c) t = fma(img[r * rs + c * cs], y[c], t);
+  zp_row(db, slot, 2 * jt)[jt * TS + r] = t;
+  zp_row(db, slot, 2 * jt + 1)[jt * TS + r] = 0.0;
+}
+
 // ---------------------------------------------------------------------------------------------
 // Wave GEMM core:  acc[a][b] += A(64 x K) * B(32 x K)^T
 //   A rows r0..r0+63 with element (r, k) at A[r + k*lda] (column-major; rows contiguous); B rows
@@ -273,6 +306,37 @@ __device__ __forceinline__ void acc4_zero(d4 (&acc)[QM][QN]) {
     for (int b = 0; b < QN; ++b) acc[a][b] = (d4){0.0, 0.0, 0.0, 0.0};
 }
 
+// z = L^-1 y fused into the producers of L^-1: every L^-1 tile (ti, tj) (written exactly once, by
+// a diagonal kernel, the leaf or LINV21) also writes its 64-row partial  L^-1[ti,tj] y[tj]  into
+// zp[slot][2 tj + half][ti*64 + r] (half: 32-column halves of the pair-unit GEMM; 64-column
+// producers write half 0 and zero half 1).  k_alpha phase 0 then sums <= 2(ti+1) partials per row
+// instead of re-reading L^-1 from HBM.
+// 64 x 64 accumulator tile (mma_64x64 layout) of sgn * L^-1[ti,tj]
+__device__ __forceinline__ void zp_acc4(const DevBatch& db, int slot, int ti, int tj, const d4 (&acc)[QM][QN], double sgn) {
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  const double* y = db.Y + (size_t)slot * db.Npad + tj * TS;
+  double yv[QN][4];
+#pragma unroll
+  for (int b = 0; b < QN; ++b)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) yv[b][q] = y[16 * b + lk + 4 * q];
+  double* z0 = zp_row(db, slot, 2 * tj) + ti * TS;
+  double* z1 = zp_row(db, slot, 2 * tj + 1) + ti * TS;
+#pragma unroll
+  for (int a = 0; a < QM; ++a) {
+    double t = 0.0;
+#pragma unroll
+    for (int b = 0; b < QN; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) t = fma(acc[a][b][q], yv[b][q], t);
+    t += __shfl_xor(t, 16);
+    t += __shfl_xor(t, 32);
+    if (lk == 0) {
+      z0[16 * a + lr] = sgn * t;
+      z1[16 * a + lr] = 0.0;
+    }
+  }
+}
 // Units of the 4-wave workgroups of k_gemm / k_lauum_grad: UR x UC output tiles (UR UC = 4), wave w
 // = tile (pr + w / UC, pc + w % UC).  The shape follows the op so that the four waves of a unit
 // share one K range where it varies by tile: TRSM (K grows with the column) 4 x 1, TT / LINV21 (K
@@ -534,6 +598,7 @@ __device__ __forceinline__ void diag_tile(const DevBatch& db, int slot, int jt) 
     Li[(size_t)c * ld + r] = Ls[c * DS + r];  // Linv[r][c] = X[r][c]
     Mj[(size_t)c * ld + r] = Ls[r * DS + c];  // Mt[r][c]   = X[c][r]
   }
+  zp_diag(db, slot, jt, Ls, 1, DS);
 }
 __global__ __launch_bounds__(NTHR) void k_diag(DevBatch db, int jt) { diag_tile(db, blockIdx.x, jt); }
 __device__ __forceinline__ void diag_tile_fast(const DevBatch& db, int slot, int jt);
@@ -722,6 +787,7 @@ __device__ __forceinline__ void diag_tile_fast(const DevBatch& db, int slot, int
     Li[(size_t)c * ld + r] = v;                              // Linv[r][c]
     Mj[(size_t)c * ld + r] = (c >= r) ? Xi[r * FS + c] : 0.0;  // Mt[r][c] = X[c][r]
   }
+  zp_diag(db, slot, jt, Xi, 1, FS, cbs);
 }
 
 
@@ -855,6 +921,7 @@ __device__ __forceinline__ void diag_wave(const DevBatch& db, int slot, int jt, 
     Mj[(size_t)q * ld + r] = T[q * CS + r];  // Mt[c=r][r'=q] = X[q][r]
     Li[(size_t)q * ld + r] = T[r * CS + q];  // Linv[r][q]    = X[r][q]
   }
+  zp_diag(db, slot, jt, T, CS, 1);
 }
 __global__ __launch_bounds__(64) void k_diag_w(DevBatch db, int jt) {
   __shared__ __attribute__((aligned(16))) double sm[DWS];
@@ -935,6 +1002,7 @@ __device__ __forceinline__ void gemm_tile(const DevBatch& db, const GemmGeom& g,
         double* p = Ct + (size_t)(16 * b + lk + 4 * q) * ld + 16 * a + lr;
         *p = (op == OP_SYRK ? -1.0 : sgn) * acc[a][b][q];  // SYRK: C - L L^T = -acc
       }
+  if (op == OP_LINV21) zp_acc4(db, slot, ti, tj, acc, -1.0);
   if (op == OP_LINV21) {  // Mt[tj, ti] = Linv[ti, tj]^T, transposed through LDS 16 rows at a time
     // so that every store instruction writes one contiguous 512-B column segment of Mt
     extern __shared__ __attribute__((aligned(16))) double gsm[];
@@ -1006,6 +1074,29 @@ __device__ __forceinline__ void gemm_body(const DevBatch& db, const GemmGeom& g1
   }
 }
 
+// 64 x 32 accumulator half-tile (mma_64x32 layout, columns 32 half ..) of sgn * L^-1[ti,tj]
+__device__ __forceinline__ void zp_acc2(const DevBatch& db, int slot, int ti, int tj, int half, const d4 (&acc)[WM][WN],
+                                        double sgn) {
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  const double* y = db.Y + (size_t)slot * db.Npad + tj * TS + 32 * half;
+  double yv[WN][4];
+#pragma unroll
+  for (int b = 0; b < WN; ++b)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) yv[b][q] = y[16 * b + lk + 4 * q];
+  double* z = zp_row(db, slot, 2 * tj + half) + ti * TS;
+#pragma unroll
+  for (int a = 0; a < WM; ++a) {
+    double t = 0.0;
+#pragma unroll
+    for (int b = 0; b < WN; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) t = fma(acc[a][b][q], yv[b][q], t);
+    t += __shfl_xor(t, 16);
+    t += __shfl_xor(t, 32);
+    if (lk == 0) z[16 * a + lr] = sgn * t;
+  }
+}
 // Small recursion nodes: unit = 2 vertically adjacent 64 x 64 tiles, wave = 64 x 32, single-stage
 // core at 4 waves/SIMD (more, shorter units than the 2 x 2 form: better for K <= 512).
 __device__ __forceinline__ void gemm_body_pair(const DevBatch& db, const GemmGeom& g1, const GemmGeom& g2) {
@@ -1096,6 +1187,7 @@ __device__ __forceinline__ void gemm_body_pair(const DevBatch& db, const GemmGeo
         if (op == OP_SYRK) *p = *p - acc[a][b][q];
         else *p = sgn * acc[a][b][q];
       }
+  if (op == OP_LINV21) zp_acc2(db, slot, ti, tj, wc, acc, -1.0);
   if (op == OP_LINV21) {  // Mt[tj, ti] = Linv[ti, tj]^T
     double* Mtt = db.Mt + so + (size_t)(ti * TS) * ld + tj * TS + 32 * wc;
 #pragma unroll
@@ -1246,6 +1338,33 @@ __device__ __forceinline__ void leaf_body(const DevBatch& db, int o, int n) {
     }
     __syncthreads();
   }
+  // z partials of the off-diagonal L^-1 tiles of this leaf, read back from L2 (this workgroup
+  // wrote them; the diagonal tiles' partials come from diag_tile_fast); <= 6 tiles, one barrier
+  __threadfence_block();
+  {
+    const int r = threadIdx.x & 63, qc = threadIdx.x >> 6;  // 4 quarters of 16 columns
+    int k = 0;
+    for (int s = 1; s < n; ++s)
+      for (int t = 0; t < n - s; ++t, ++k) {
+        const int tj = o + t, ti = tj + s;
+        const double* Lt = Li + (size_t)(tj * TS) * ld + ti * TS;
+        const double* y = db.Y + (size_t)slot * db.Npad + tj * TS;
+        double acc = 0.0;
+#pragma unroll
+        for (int c = 16 * qc; c < 16 * qc + 16; ++c) acc = fma(Lt[(size_t)c * ld + r], y[c], acc);
+        tbs[(4 * k + qc) * TS + r] = acc;  // k < 16: fits the [4][16][65] buffer
+      }
+    __syncthreads();
+    k = 0;
+    for (int s = 1; s < n; ++s)
+      for (int t = 0; t < n - s; ++t, ++k)
+        if (qc == 0) {
+          const int tj = o + t, ti = tj + s;
+          const double* pk = tbs + 4 * k * TS;
+          zp_row(db, slot, 2 * tj)[ti * TS + r] = ((pk[r] + pk[TS + r]) + pk[2 * TS + r]) + pk[3 * TS + r];
+          zp_row(db, slot, 2 * tj + 1)[ti * TS + r] = 0.0;
+        }
+  }
 }
 
 __global__ __launch_bounds__(NTHR) void k_leaf(DevBatch db, int o, int n) { leaf_body(db, o, n); }
@@ -1257,12 +1376,19 @@ __global__ __launch_bounds__(NTHR) void k_alpha(DevBatch db, int phase) {
   __shared__ double part[4][TS];
   int slot, i;
   if (!map_block(blockIdx.x, db.B, db.nt, slot, i)) return;
-  if (phase == 0) i = db.nt - 1 - i;  // longest rows first
   const int r = threadIdx.x & 63, pt = threadIdx.x >> 6;
+  if (phase == 0) {  // z = L^-1 y from the producers' partials: rows of tile i, halves h < 2(i+1)
+    double acc = 0.0;
+    for (int h = pt; h < 2 * (i + 1); h += 4) acc += zp_row(db, slot, h)[i * TS + r];
+    part[pt][r] = acc;
+    __syncthreads();
+    if (pt == 0) db.z[(size_t)slot * db.Npad + i * TS + r] = ((part[0][r] + part[1][r]) + part[2][r]) + part[3][r];
+    return;
+  }
   const size_t ld = db.ld;
-  const double* A = (phase == 0 ? db.Linv : db.Mt) + (size_t)slot * db.mat + i * TS + r;
-  const double* v = (phase == 0 ? db.Y : db.z) + (size_t)slot * db.Npad;
-  const int k0 = (phase == 0) ? 0 : i * TS, k1 = (phase == 0) ? (i + 1) * TS : db.Npad;
+  const double* A = db.Mt + (size_t)slot * db.mat + i * TS + r;
+  const double* v = db.z + (size_t)slot * db.Npad;
+  const int k0 = i * TS, k1 = db.Npad;
   // columns [k0, k1) split in 4 contiguous quarters of whole 16-column groups, 8 loads in flight
   const int ng = (k1 - k0) / 16, g0 = (ng * pt) / 4, g1 = (ng * (pt + 1)) / 4;
   double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1275,7 +1401,7 @@ __global__ __launch_bounds__(NTHR) void k_alpha(DevBatch db, int phase) {
   __syncthreads();
   if (pt == 0) {
     const double s = ((part[0][r] + part[1][r]) + part[2][r]) + part[3][r];
-    (phase == 0 ? db.z : db.alpha)[(size_t)slot * db.Npad + i * TS + r] = s;
+    db.alpha[(size_t)slot * db.Npad + i * TS + r] = s;
   }
 }
 
