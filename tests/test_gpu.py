@@ -277,3 +277,31 @@ def test_factorisation_paths_match_golden(gprx, golden_dir, monkeypatch, leaf, d
         b.close()
     finally:
         c.close()
+
+
+def test_production_path_b32_full_size(gprx, ctx):
+    """The bench's configuration: B >= 32 slots (fused 256x256 leaves, folded 64x64 GEMM units,
+    folded lauum jobs) at N=2048, d=26, M=100; three slots against the oracle, all slots finite
+    and bit-identical across repeated runs."""
+    from gprx import data
+
+    B = 32
+    trs = [data.make_trial("P2", 2048, 100, seed=data.trial_seed("P2", t)) for t in range(B // 6 + 1)]
+    X = np.stack([trs[s // 6]["X"] for s in range(B)])
+    Y = np.stack([trs[s // 6]["Y"][s % 6] for s in range(B)])
+    Xs = np.stack([trs[s // 6]["Xs"] for s in range(B)])
+    rng = np.random.default_rng(5)
+    th0 = data.theta0("P2", 2048)
+    T = np.stack([th0 + 0.05 * rng.standard_normal(th0.shape[0]) for _ in range(B)])
+    b = gprx.GPBatch(B, 26, 2048, 100, ctx=ctx)
+    b.set_train(X, Y)
+    b.set_test(Xs)
+    r1 = b.run(T, grad=True, predict=True)
+    r2 = b.run(T, grad=True, predict=True)
+    assert np.all(r1["status"] == 0)
+    for k in ("mll", "grad", "mu", "var"):
+        assert np.all(np.isfinite(r1[k]))
+        np.testing.assert_array_equal(r1[k], r2[k])
+    for s in (0, 13, 31):
+        check_slot(r1, s, X[s], Y[s], T[s], Xs[s], 0)
+    b.close()
