@@ -1099,12 +1099,23 @@ __device__ __forceinline__ void zp_acc2(const DevBatch& db, int slot, int ti, in
 }
 // Small recursion nodes: unit = 2 vertically adjacent 64 x 64 tiles, wave = 64 x 32, single-stage
 // core at 4 waves/SIMD (more, shorter units than the 2 x 2 form: better for K <= 512).
+__device__ __forceinline__ void gemm_tile_pair(const DevBatch& db, const GemmGeom& g, int slot, int ti, int tj, int wc);
+// units: tri (SYRK) as pair_unit; TRSM folds column c with C-1-c; TT / LINV21 / PREDVAR fold
+// row pair p with P-1-p (the folding of gemm_body, for 2 x 1 units)
+__host__ __device__ inline int pair_op_units(const GemmGeom& g, int nt, int mt) {
+  int r0, c0, R, C;
+  bool tri;
+  op_rect(g, nt, mt, r0, c0, R, C, tri);
+  if (tri || g.op == OP_SYRK) return pair_units(R, C, tri);
+  const int P = (R + 1) / 2;
+  return g.op == OP_TRSM ? P * ((C + 1) / 2) : ((P + 1) / 2) * C;
+}
 __device__ __forceinline__ void gemm_body_pair(const DevBatch& db, const GemmGeom& g1, const GemmGeom& g2) {
   int r0, c0, R, C, r02, c02, R2, C2;
   bool tri, tri2;
   op_rect(g1, db.nt, db.mt, r0, c0, R, C, tri);
   op_rect(g2, db.nt, db.mt, r02, c02, R2, C2, tri2);
-  const int T1 = pair_units(R, C, tri), T2 = g2.op == OP_NONE ? 0 : pair_units(R2, C2, tri2);
+  const int T1 = pair_op_units(g1, db.nt, db.mt), T2 = g2.op == OP_NONE ? 0 : pair_op_units(g2, db.nt, db.mt);
   int slot, u, pr, pc;
   if (!map_block(blockIdx.x, db.B, T1 + T2, slot, u)) return;
   const GemmGeom g = u < T1 ? g1 : g2;  // block-uniform
@@ -1113,22 +1124,37 @@ __device__ __forceinline__ void gemm_body_pair(const DevBatch& db, const GemmGeo
     r0 = r02; c0 = c02; R = R2; C = C2; tri = tri2;
   }
   const int op = g.op;
-  // longest K range first (the tail of a launch is its longest units)
+  int np = 1, pr2 = 0, pc2 = 0;
   if (tri) {
     pair_unit(u, R, C, tri, pr, pc);
-  } else {
-    const int P = (R + 1) / 2;
-    const int pi = u / C;
+  } else if (op == OP_SYRK) {
+    const int P = (R + 1) / 2, pi = u / C;
+    pr = 2 * (P - 1 - pi);
     pc = u - pi * C;
-    switch (op) {
-      case OP_TRSM: pc = C - 1 - pc; pr = 2 * pi; break;      // K grows with the column
-      case OP_TT: pr = 2 * pi; break;                           // K shrinks with the row
-      default: pr = 2 * (P - 1 - pi); break;                    // LINV21 / PREDVAR: K grows with the row
-    }
+  } else if (op == OP_TRSM) {  // K grows with the column: fold columns
+    const int nf = (C + 1) / 2, pi = u / nf, f = u - pi * nf;
+    pr = pr2 = 2 * pi;
+    pc = C - 1 - f;
+    pc2 = f;
+    np = (pc != pc2) ? 2 : 1;
+  } else {  // fold row pairs; TT: K shrinks with the row, LINV21 / PREDVAR: K grows with the row
+    const int P = (R + 1) / 2, f = u / C;
+    pc = pc2 = u - f * C;
+    const int lo = f, hi = P - 1 - f;
+    pr = 2 * (op == OP_TT ? lo : hi);
+    pr2 = 2 * (op == OP_TT ? hi : lo);
+    np = (lo != hi) ? 2 : 1;
   }
-  const int w = threadIdx.x >> 6, wr = w >> 1, wc = w & 1;
-  if (pr + wr >= R) return;  // wave-uniform: second tile of an odd pair
-  const int ti = r0 + pr + wr, tj = c0 + pc;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), wr = w >> 1, wc = w & 1;
+#pragma unroll 1
+  for (int pass = 0; pass < np; ++pass) {
+    const int ur = pass ? pr2 : pr, uc = pass ? pc2 : pc;
+    if (ur + wr >= R) continue;  // wave-uniform: second tile of an odd pair
+    gemm_tile_pair(db, g, slot, __builtin_amdgcn_readfirstlane(r0 + ur + wr), __builtin_amdgcn_readfirstlane(c0 + uc), wc);
+  }
+}
+__device__ __forceinline__ void gemm_tile_pair(const DevBatch& db, const GemmGeom& g, int slot, int ti, int tj, int wc) {
+  const int op = g.op;
   const size_t ld = db.ld, so = (size_t)slot * db.mat;
   int kb, ke;  // K range in tiles
   const double *A, *Bm;
@@ -1188,7 +1214,7 @@ __device__ __forceinline__ void gemm_body_pair(const DevBatch& db, const GemmGeo
         else *p = sgn * acc[a][b][q];
       }
   if (op == OP_LINV21) zp_acc2(db, slot, ti, tj, wc, acc, -1.0);
-  if (op == OP_LINV21) {  // Mt[tj, ti] = Linv[ti, tj]^T
+  if (op == OP_LINV21) {  // Mt[tj, ti] = Linv[ti, tj]^T (direct: an LDS transpose measured slower here)
     double* Mtt = db.Mt + so + (size_t)(ti * TS) * ld + tj * TS + 32 * wc;
 #pragma unroll
     for (int a = 0; a < WM; ++a)
@@ -1839,14 +1865,8 @@ void launch_leaf(const DevBatch& b, int o, int n, hipStream_t s) {
 }
 void launch_gemm(const DevBatch& b, const GemmGeom& g, hipStream_t s, const GemmGeom& g2) {
   if (g.op != OP_PREDVAR && g.n <= b.small_n) {  // small node: pair units, 64 x 32 waves
-    int r0, c0, R, C;
-    bool tri;
-    op_rect(g, b.nt, b.mt, r0, c0, R, C, tri);
-    int T = pair_units(R, C, tri);
-    if (g2.op != OP_NONE) {
-      op_rect(g2, b.nt, b.mt, r0, c0, R, C, tri);
-      T += pair_units(R, C, tri);
-    }
+    int T = pair_op_units(g, b.nt, b.mt);
+    if (g2.op != OP_NONE) T += pair_op_units(g2, b.nt, b.mt);
     hipLaunchKernelGGL(k_gemm_p, dim3(grid_blocks(b.B, T)), dim3(NTHR), 0, s, b, g, g2);
     return;
   }
