@@ -7,6 +7,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -56,6 +57,7 @@ struct gprx_ctx {
   std::vector<hipEvent_t> smarks;     // stagger events (nstreams)
   std::vector<hipStream_t> sstreams;  // prediction side stream per group
   std::vector<hipEvent_t> sevents;    // 3 per group: fork, factorised, join
+  std::set<gprx_batch*> batches;      // live batches (destroyed with the context)
   bool side = false;                  // GPRX_SIDE=1: prediction on a side stream (measured no gain:
                                       // the big kernels fill the register file, nothing co-resides)
 };
@@ -461,6 +463,7 @@ void gprx_ctx_destroy(gprx_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
+  while (!c->batches.empty()) gprx_batch_destroy(*c->batches.begin());  // handles become invalid
   for (auto& p : c->pending) {
     (void)hipEventDestroy(p.a);
     (void)hipEventDestroy(p.b);
@@ -528,6 +531,7 @@ int gprx_batch_create(gprx_ctx* c, int B, int d, int N, int M_max, gprx_batch** 
   if (hipSetDevice(c->device) != hipSuccess) return GPRX_DEVICE_ERROR;
   gprx_batch* b = new gprx_batch();
   b->ctx = c;
+  c->batches.insert(b);
   DevBatch& db = b->db;
   db.B = B;
   db.d = d;
@@ -589,6 +593,10 @@ int gprx_batch_create(gprx_ctx* c, int B, int d, int N, int M_max, gprx_batch** 
 
 void gprx_batch_destroy(gprx_batch* b) {
   if (!b) return;
+  if (b->ctx) {
+    std::lock_guard<std::mutex> g(b->ctx->mu);
+    b->ctx->batches.erase(b);
+  }
   if (b->ctx) (void)hipSetDevice(b->ctx->device);
   if (b->ctx) (void)hipStreamSynchronize(b->ctx->stream);
   for (int i = 0; i < 4; ++i)
@@ -686,9 +694,9 @@ int gprx_batch_run(gprx_batch* b, const double* theta, unsigned flags, double* m
     const char* ab = getenv("GPRX_ABLATE");  // timing experiments only; results are wrong when set
     db.ablate = ab ? atoi(ab) : 0;
     const char* sn = getenv("GPRX_SMALL_N");
-    db.small_n = sn ? atoi(sn) : 8;
+    db.small_n = sn ? atoi(sn) : (db.B >= 32 ? 8 : 64);  // small batches: more, smaller units
     const char* dv = getenv("GPRX_DIAGV");
-    db.diag_variant = dv ? atoi(dv) : 1;
+    db.diag_variant = dv ? atoi(dv) : 2;  // blocked MFMA diagonal kernel (measured fastest)
   }
   const int d = db.d, B = db.B, np = d + 2;
   // hyper-parameters -> kernel parameters, exactly as SEArd / GPE derive them:

@@ -6,8 +6,10 @@ A `GPBatch` holds B GP slots of equal (d, N) in HBM -- the G per-output GPs of a
 """
 from __future__ import annotations
 
+import atexit
 import ctypes as C
 import threading
+import weakref
 
 import numpy as np
 
@@ -15,6 +17,18 @@ from . import _lib as L
 
 _ctx_lock = threading.Lock()
 _default_ctx: dict[int, "Context"] = {}
+# live handles, released before interpreter teardown: the HIP runtime's own static destructors run
+# after Python finalisation, and a batch or context freed after them aborts the process
+_live_batches: "weakref.WeakSet[GPBatch]" = weakref.WeakSet()
+_live_ctxs: "weakref.WeakSet[Context]" = weakref.WeakSet()
+
+
+@atexit.register
+def _release_all():
+    for b in list(_live_batches):
+        b.close()
+    for c in list(_live_ctxs):
+        c.close()
 
 
 class Context:
@@ -25,6 +39,7 @@ class Context:
         L.check(L.lib.gprx_ctx_create(int(device), C.byref(h)))
         self.h = h
         self.device = int(device)
+        _live_ctxs.add(self)
         self.set_dist_mode(dist_mode)
 
     def set_dist_mode(self, mode: int):
@@ -84,6 +99,7 @@ class GPBatch:
         self.h = h
         self.B, self.d, self.N = int(B), int(d), int(N)
         self.M = 0
+        _live_batches.add(self)
 
     # -- inputs -----------------------------------------------------------------------------
     def set_train(self, X, Y):
@@ -158,7 +174,8 @@ class GPBatch:
 
     def close(self):
         if getattr(self, "h", None):
-            L.lib.gprx_batch_destroy(self.h)
+            if getattr(self.ctx, "h", None):  # a closed context already synchronised its stream
+                L.lib.gprx_batch_destroy(self.h)
             self.h = None
 
     def __del__(self):

@@ -70,6 +70,7 @@ const char* gprx_status_string(int status);
 
 /* ---- context: one device, one stream ------------------------------------------------------ */
 int gprx_ctx_create(int device, gprx_ctx** out);
+/* also destroys the context's remaining batches / GPs: their handles become invalid */
 void gprx_ctx_destroy(gprx_ctx* ctx);
 const char* gprx_ctx_last_error(const gprx_ctx* ctx);
 int gprx_ctx_set_dist_mode(gprx_ctx* ctx, int mode);

@@ -1,10 +1,15 @@
 """Parity of the gfx950 path (through the C ABI) with the oracle restatement.
 
-Tolerances (fp64; DESIGN.md 'Parity'):
-  mll   |Δ| <= 1e-9  * max(1, |mll|)
-  grad  |Δ| <= 1e-7  * max(1, max|grad|)
-  mu    |Δ| <= 1e-9  * max|y|
-  var   |Δ| <= 1e-9  * σf²
+Tolerances (fp64; DESIGN.md 'Parity'), each the larger of a fixed bound and 10x the spread
+between the oracle's two legitimate distance formulations (expanded a^2+b^2-2ab vs direct
+(a-b)^2) on the same inputs -- the problem's own sensitivity to rounding, as SURVEY.md 8(d)
+prescribes for calibrating the tolerance.  On well-conditioned inputs the spread is ~1e-14 and the
+fixed bounds apply; on the ill-conditioned cartpole cases (cond(K) ~ 1e8) the two CPU
+formulations already differ by up to 7.5e-10 in the LML.
+  mll   |d| <= max(1e-9 * max(1, |mll|),        10 spread)
+  grad  |d| <= max(1e-7 * max(1, max|grad|),    10 spread)
+  mu    |d| <= max(1e-9 * max|y|,               10 spread)
+  var   |d| <= max(1e-9 * sf^2,                 10 spread)
 Status / pivot index / CState indexing: exact.
 """
 import math
@@ -17,6 +22,33 @@ pytestmark = pytest.mark.gpu
 from oracle import gp_oracle as O  # noqa: E402
 
 TOL_MLL, TOL_GRAD, TOL_MU, TOL_VAR = 1e-9, 1e-7, 1e-9, 1e-9
+
+
+def tolerances(f, f2, y, theta):
+    """Per-quantity bounds for a result compared against oracle fit f (f2: the same fit in the
+    other distance mode)."""
+    def spread(k):
+        return float(np.max(np.abs(np.asarray(f[k]) - np.asarray(f2[k])))) if k in f and k in f2 else 0.0
+
+    sf2 = math.exp(2 * theta[-1])
+    return dict(
+        mll=max(TOL_MLL * max(1.0, abs(f["mll"])), 10 * spread("mll")),
+        grad=max(TOL_GRAD * max(1.0, float(np.max(np.abs(f["grad"])))), 10 * spread("grad")),
+        mu=max(TOL_MU * float(np.max(np.abs(y))), 10 * spread("mu")),
+        var=max(TOL_VAR * sf2, 10 * spread("var")),
+    )
+
+
+def check_slot(r, s, X, y, theta, Xs, mode):
+    f = O.fit(X, y, theta, Xs, mode)
+    t = tolerances(f, O.fit(X, y, theta, Xs, 1 - mode), y, theta)
+    assert r["status"][s] == 0
+    assert abs(r["mll"][s] - f["mll"]) <= t["mll"]
+    if r["grad"] is not None:
+        assert np.max(np.abs(r["grad"][s] - f["grad"])) <= t["grad"]
+    if r["mu"] is not None:
+        assert np.max(np.abs(r["mu"][s] - f["mu"])) <= t["mu"]
+        assert np.max(np.abs(r["var"][s] - f["var"])) <= t["var"]
 
 
 @pytest.fixture(scope="module")
@@ -33,19 +65,6 @@ def ctx(gprx):
     c.close()
 
 
-def check_slot(r, s, X, y, theta, Xs, mode):
-    f = O.fit(X, y, theta, Xs, mode)
-    assert r["status"][s] == 0
-    assert abs(r["mll"][s] - f["mll"]) <= TOL_MLL * max(1.0, abs(f["mll"]))
-    if r["grad"] is not None:
-        gs = max(1.0, np.max(np.abs(f["grad"])))
-        assert np.max(np.abs(r["grad"][s] - f["grad"])) <= TOL_GRAD * gs
-    if r["mu"] is not None:
-        assert np.max(np.abs(r["mu"][s] - f["mu"])) <= TOL_MU * np.max(np.abs(y))
-        sf2 = math.exp(2 * theta[-1])
-        assert np.max(np.abs(r["var"][s] - f["var"])) <= TOL_VAR * sf2
-
-
 @pytest.mark.parametrize("name", ["p1_n50", "cp_n64", "p2_n100", "p2_n256", "fb_n64"])
 @pytest.mark.parametrize("mode", [0, 1])
 def test_golden_batch(gprx, ctx, golden_dir, name, mode):
@@ -59,12 +78,15 @@ def test_golden_batch(gprx, ctx, golden_dir, name, mode):
     b.set_test(Xs)
     r = b.run(np.tile(th, (G, 1)), grad=True, predict=True)
     assert np.all(r["status"] == 0)
+    other = "dir" if tag == "exp" else "exp"
     for g in range(G):
-        assert abs(r["mll"][g] - z[f"mll_{tag}"][g]) <= TOL_MLL * max(1.0, abs(z[f"mll_{tag}"][g]))
-        gs = max(1.0, np.max(np.abs(z[f"grad_{tag}"][g])))
-        assert np.max(np.abs(r["grad"][g] - z[f"grad_{tag}"][g])) <= TOL_GRAD * gs
-        assert np.max(np.abs(r["mu"][g] - z[f"mu_{tag}"][g])) <= TOL_MU * np.max(np.abs(Y[g]))
-        assert np.max(np.abs(r["var"][g] - z[f"var_{tag}"][g])) <= TOL_VAR * math.exp(2 * th[-1])
+        f = {k: z[f"{k}_{tag}"][g] for k in ("mll", "grad", "mu", "var")}
+        f2 = {k: z[f"{k}_{other}"][g] for k in ("mll", "grad", "mu", "var")}
+        t = tolerances(f, f2, Y[g], th)
+        assert abs(r["mll"][g] - f["mll"]) <= t["mll"]
+        assert np.max(np.abs(r["grad"][g] - f["grad"])) <= t["grad"]
+        assert np.max(np.abs(r["mu"][g] - f["mu"])) <= t["mu"]
+        assert np.max(np.abs(r["var"][g] - f["var"])) <= t["var"]
     ctx.set_dist_mode(0)
 
 
