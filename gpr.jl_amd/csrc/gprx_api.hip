@@ -289,6 +289,7 @@ void predict_cross(gprx_ctx* c, hipStream_t st, const DevBatch& db) {
         [&] { gprx::launch_pred_cross(db, st); });
 }
 void predict_var(gprx_ctx* c, hipStream_t st, const DevBatch& db) {
+  if (!db.want_var) return;
   const double N = db.N, M = db.M, B = db.B;
   gprx::GemmGeom g{gprx::OP_PREDVAR, 0, 0, 0};
   timed(c, st, "pred_var", B * N * N * M, B * 8.0 * (N * N / 2 + N * db.Mpad), [&] { gprx::launch_gemm(db, g, st); });
@@ -668,6 +669,7 @@ static int batch_predict_locked(gprx_batch* b, double* mu, double* var) {
   DevBatch& db = b->db;
   if (!b->factored) return set_err(c, GPRX_NOT_READY, "predict before a successful factorisation");
   if (!b->have_test || db.M == 0) return GPRX_OK;
+  db.want_var = var != nullptr;
   int rc = run_groups(b, false, true, false);
   if (rc) return rc;
   HIPCHK(c, hipMemcpyAsync(b->h_mu, db.out_mu, (size_t)db.B * db.Mpad * sizeof(double), hipMemcpyDeviceToHost, c->stream));
@@ -690,6 +692,7 @@ int gprx_batch_run(gprx_batch* b, const double* theta, unsigned flags, double* m
   if (hipSetDevice(c->device) != hipSuccess) return GPRX_DEVICE_ERROR;
   DevBatch& db = b->db;
   db.dist_mode = c->dist_mode;
+  db.want_var = var != nullptr;
   {
     const char* ab = getenv("GPRX_ABLATE");  // timing experiments only; results are wrong when set
     db.ablate = ab ? atoi(ab) : 0;

@@ -22,6 +22,8 @@ struct DevBatch {
   int B, d, N, Npad, nt, ntl;  // nt = Npad/64 tiles per edge, ntl = nt(nt+1)/2 lower tiles
   int M, Mpad, mt;             // test points (per slot), padded to 64, mt = Mpad/64
   int dist_mode;               // GPRX_DIST_EXPANDED / GPRX_DIST_DIRECT
+  int want_var;                // predictive variance requested (var output non-NULL); 0 skips the
+                               // O(N^2 M) variance GEMM (predictdynamics.jl uses the mean only)
   int ablate;                  // timing-only ablation bits (env GPRX_ABLATE; 0 in production)
   int small_n;                 // recursion nodes of <= small_n tiles use the 64 x 32 pair-unit GEMM
                                // (GPRX_SMALL_N; default 8 for B >= 32, all nodes below that, where

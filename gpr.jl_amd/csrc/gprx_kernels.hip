@@ -1821,11 +1821,11 @@ __global__ __launch_bounds__(NTHR) void k_pred_final(DevBatch db) {
     double mu = 0.0, s = 0.0;
     for (int k = 0; k < db.nt; ++k) {
       mu += db.mu_part[((size_t)slot * db.nt + k) * db.Mpad + m];
-      s += db.var_part[((size_t)slot * db.nt + k) * db.Mpad + m];
+      if (db.want_var) s += db.var_part[((size_t)slot * db.nt + k) * db.Mpad + m];
     }
     const double v = sf2 - s;
     db.out_mu[(size_t)slot * db.Mpad + m] = mu;
-    db.out_var[(size_t)slot * db.Mpad + m] = v > 0.0 ? v : 0.0;
+    db.out_var[(size_t)slot * db.Mpad + m] = db.want_var ? (v > 0.0 ? v : 0.0) : 0.0;
   }
 }
 

@@ -146,8 +146,10 @@ class GPBatch:
         self.M = int(M)
 
     # -- evaluation ---------------------------------------------------------------------------
-    def run(self, theta, grad: bool = True, predict: bool = False, raise_on_error: bool = False):
-        """Returns dict(mll[B], grad[B,d+2] | None, mu[B,M] | None, var[B,M] | None, status[B], info[B])."""
+    def run(self, theta, grad: bool = True, predict: bool = False, raise_on_error: bool = False,
+            variance: bool = True):
+        """Returns dict(mll[B], grad[B,d+2] | None, mu[B,M] | None, var[B,M] | None, status[B], info[B]).
+        variance=False skips the predictive variance (its O(N^2 M) GEMM); var is then None."""
         theta = _f64(theta)
         if theta.ndim == 1:
             theta = np.broadcast_to(theta, (self.B, self.d + 2)).copy()
@@ -156,7 +158,7 @@ class GPBatch:
         g = np.empty((self.B, self.d + 2)) if grad else None
         pred = predict and self.M > 0
         mu = np.empty((self.B, self.M)) if pred else None
-        var = np.empty((self.B, self.M)) if pred else None
+        var = np.empty((self.B, self.M)) if pred and variance else None
         st = np.empty(self.B, dtype=np.int32)
         info = np.empty(self.B, dtype=np.int32)
         flags = (L.WANT_GRAD if grad else 0) | (L.WANT_PREDICT if pred else 0)
@@ -166,9 +168,11 @@ class GPBatch:
             L.check(rc, self.ctx.h)
         return dict(mll=mll, grad=g, mu=mu, var=var, status=st, info=info)
 
-    def predict(self):
+    def predict(self, variance: bool = True):
+        """Predictive mean (and variance) at the current test points from the last run's
+        factorisation; variance=False returns (mu, None) without the variance GEMM."""
         mu = np.empty((self.B, self.M))
-        var = np.empty((self.B, self.M))
+        var = np.empty((self.B, self.M)) if variance else None
         L.check(L.lib.gprx_batch_predict(self.h, L.dptr(mu), L.dptr(var)), self.ctx.h)
         return mu, var
 

@@ -169,6 +169,18 @@ class GPE:
         mu, var = self.predict_f(xs)
         return mu + self.mean.mean(xs), var + math.exp(2.0 * self.logNoise)
 
+    def predict_y_mean(self, xs):
+        """predict_y(gp, obs)[1] without the variance: the rollout call of
+        examples/utils/predictdynamics.jl:13 (uses the mean only); skips the O(N^2 M) variance."""
+        xs = np.asarray(xs, dtype=np.float64)
+        if xs.ndim == 1:
+            xs = xs[:, None]
+        if xs.shape[0] != self.dim:
+            raise ValueError("test inputs have the wrong dimension")
+        self._batch.set_test(xs)
+        mu, _ = self._batch.predict(variance=False)
+        return mu[0] + self.mean.mean(xs)
+
 
 def GP(x, y, mean, kernel, logNoise: float = -2.0, ctx: Context | None = None) -> GPE:
     """GaussianProcesses.GP(x, y, mean, kernel[, logNoise])."""

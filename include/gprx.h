@@ -94,12 +94,15 @@ int gprx_batch_set_train(gprx_batch* batch, const double* X, int64_t x_slot_stri
 int gprx_batch_set_test(gprx_batch* batch, const double* Xs, int M, int64_t xs_slot_stride, int mem);
 /* Evaluate every slot at theta[b*(d+2) ...]: Gram build, Cholesky, alpha, log marginal
  * likelihood; optionally its gradient and the predictive mean/variance (f-space: no noise, no
- * prior mean) at the test points.  Outputs (host pointers, any may be NULL):
+ * prior mean) at the test points.  var == NULL skips the O(N^2 M) variance computation (the
+ * rollout pattern of predictdynamics.jl:13, which uses the mean only).  Outputs (host pointers,
+ * any may be NULL):
  *   mll[B], grad[B*(d+2)], mu[B*M], var[B*M], status[B], info[B] (1-based failing pivot).
  * Returns GPRX_OK when every slot succeeded, otherwise the first failing slot's status.          */
 int gprx_batch_run(gprx_batch* batch, const double* theta, unsigned flags, double* mll, double* grad,
                    double* mu, double* var, int* status, int* info);
-/* Predictive mean/variance from the factorisation of the last gprx_batch_run (f-space).       */
+/* Predictive mean/variance from the factorisation of the last gprx_batch_run (f-space);
+ * var == NULL: mean only.                                                                      */
 int gprx_batch_predict(gprx_batch* batch, double* mu, double* var);
 int gprx_batch_dims(const gprx_batch* batch, int* B, int* d, int* N, int* M_max);
 

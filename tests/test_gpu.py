@@ -327,3 +327,27 @@ def test_production_path_b32_full_size(gprx, ctx):
     for s in (0, 13, 31):
         check_slot(r1, s, X[s], Y[s], T[s], Xs[s], 0)
     b.close()
+
+
+def test_mean_only_prediction_matches_full(gprx, ctx, golden_dir):
+    """var == NULL skips the variance GEMM; the means are bit-identical to the full prediction
+    (GPE predict_y_mean: the predictdynamics.jl:13 rollout call)."""
+    z = np.load(golden_dir / "p2_n256.npz")
+    X, Y, th, Xs = z["X"], z["Y"], z["theta"], z["Xs"]
+    G = Y.shape[0]
+    b = gprx.GPBatch(G, X.shape[0], X.shape[1], Xs.shape[1], ctx=ctx)
+    b.set_train(X, Y)
+    b.set_test(Xs)
+    full = b.run(np.tile(th, (G, 1)), grad=False, predict=True)
+    mean_only = b.run(np.tile(th, (G, 1)), grad=False, predict=True, variance=False)
+    assert mean_only["var"] is None
+    np.testing.assert_array_equal(full["mu"], mean_only["mu"])
+    mu2, var2 = b.predict(variance=False)
+    assert var2 is None
+    np.testing.assert_array_equal(mu2, full["mu"])
+    mu3, var3 = b.predict()
+    np.testing.assert_array_equal(var3, full["var"])
+    b.close()
+    gp = gprx.GP(X, Y[1], gprx.MeanZero(), gprx.SEArd(th[1:-1], th[-1]), ctx=ctx)
+    m_full, _ = gp.predict_y(Xs)
+    np.testing.assert_array_equal(gp.predict_y_mean(Xs), m_full)
