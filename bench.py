@@ -140,17 +140,21 @@ def main():
     import torch
 
     dist = None
+    ndev = torch.cuda.device_count()
+    dev = local % max(1, ndev)  # rehearsal with more ranks than GPUs shares a device
+    torch.cuda.set_device(dev)
+    backend = "nccl"
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
-    else:
-        torch.cuda.set_device(local)
+        # the collectives here are control plane only (barrier, max of the timings); RCCL when every
+        # rank has its own GPU, gloo for a shared-device rehearsal
+        backend = "nccl" if ndev >= world else "gloo"
+        dist.init_process_group(backend)
 
     import gprx
 
-    ctx = gprx.Context(local)
+    ctx = gprx.Context(dev)
     X, Y, T, XT = make_workload(args.trials, rank, world)
     B, d = X.shape[0], X.shape[1]
     batch = gprx.GPBatch(B, d, N, M, ctx=ctx)
@@ -174,7 +178,7 @@ def main():
     dt = time.perf_counter() - t0
     ok = ok and bool(np.all(r["status"] == 0))
     if dist is not None:
-        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
+        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{dev}" if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     fits = B * args.steps * world
@@ -221,7 +225,7 @@ def main():
         barrier()
         t_opt = time.perf_counter() - t0
         if dist is not None:
-            t = torch.tensor([t_opt], dtype=torch.float64, device=f"cuda:{local}")
+            t = torch.tensor([t_opt], dtype=torch.float64, device=f"cuda:{dev}" if backend == "nccl" else "cpu")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             t_opt = float(t.item())
         opt = {"value": round(B * world / t_opt, 3), "unit": "optimised GP fits/s", "max_evals_per_gp": args.opt_evals,
