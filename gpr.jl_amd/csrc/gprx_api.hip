@@ -58,6 +58,8 @@ struct gprx_ctx {
   std::vector<hipStream_t> sstreams;  // prediction side stream per group
   std::vector<hipEvent_t> sevents;    // 3 per group: fork, factorised, join
   std::set<gprx_batch*> batches;      // live batches (destroyed with the context)
+  void* rbuf = nullptr;               // rollout argument buffer (device), grown on demand
+  size_t rcap = 0;
   bool side = false;                  // GPRX_SIDE=1: prediction on a side stream (measured no gain:
                                       // the big kernels fill the register file, nothing co-resides)
 };
@@ -481,6 +483,7 @@ void gprx_ctx_destroy(gprx_ctx* c) {
     (void)hipStreamDestroy(st);
   }
   for (auto e : c->sevents) (void)hipEventDestroy(e);
+  if (c->rbuf) (void)hipFree(c->rbuf);
   (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -802,6 +805,81 @@ int gprx_gp_predict(gprx_gp* gp, const double* Xs, int M, double* mu, double* va
   if (rc) return rc;
   return gprx_batch_predict(gp->batch, mu, var);
 }
+
+// ---- rollout in minimal coordinates ------------------------------------------------------------
+int gprx_rollout_min(gprx_ctx* c, int mech, int usesin, double dt, int steps, int ngroups,
+                     gprx_batch* const* batches, const int* slots, int T, const int* traj_group,
+                     const double* start, double* final_state) {
+  if (!c) return GPRX_INVALID_ARGUMENT;
+  if (mech < GPRX_MECH_P1 || mech > GPRX_MECH_FB || steps < 0 || ngroups < 1 || T < 0 || !std::isfinite(dt))
+    return set_err(c, GPRX_INVALID_ARGUMENT, "gprx_rollout_min: bad mechanism / steps / groups / dt");
+  if (T == 0) return GPRX_OK;
+  if (!batches || !slots || !traj_group || !start || !final_state)
+    return set_err(c, GPRX_INVALID_ARGUMENT, "gprx_rollout_min: null argument");
+  // coordinates (q, qdot) per mechanism: P1 theta; P2 theta1, theta2 (relative); CP x, theta;
+  // FB theta1, theta3 -- the angle coordinates get (sin, cos) features when usesin
+  const int nc = mech == GPRX_MECH_P1 ? 1 : 2;
+  const int ang0 = mech == GPRX_MECH_CP ? 0 : 1, ang1 = nc > 1 ? 1 : 0;
+  const int dobs = (usesin && ang0 ? 3 : 2) + (nc > 1 ? (usesin && ang1 ? 3 : 2) : 0);
+  std::lock_guard<std::mutex> g(c->mu);
+  std::vector<gprx::RolloutGP> gps((size_t)ngroups * nc);
+  for (size_t k = 0; k < gps.size(); ++k) {
+    gprx_batch* b = batches[k];
+    const int s = slots[k];
+    if (!b || b->ctx != c || s < 0 || s >= b->db.B)
+      return set_err(c, GPRX_INVALID_ARGUMENT, "gprx_rollout_min: GP " + std::to_string(k) + " is not a slot of a batch of this context");
+    if (b->db.d != dobs)
+      return set_err(c, GPRX_INVALID_ARGUMENT, "gprx_rollout_min: input dimension " + std::to_string(b->db.d) + " != " + std::to_string(dobs) + " for this mechanism / usesin");
+    if (!b->factored) return set_err(c, GPRX_NOT_READY, "gprx_rollout_min: batch not factorised (run it first)");
+    if (b->h_status[s] != 0) return set_err(c, b->h_status[s], "gprx_rollout_min: slot " + std::to_string(s) + " failed its last evaluation");
+    const DevBatch& db = b->db;
+    gps[k] = gprx::RolloutGP{db.X + (size_t)s * db.Npad * db.d, db.alpha + (size_t)s * db.Npad, db.params + (size_t)s * db.pst, db.N, 0};
+  }
+  for (int t = 0; t < T; ++t)
+    if (traj_group[t] < 0 || traj_group[t] >= ngroups) return set_err(c, GPRX_INVALID_ARGUMENT, "gprx_rollout_min: trajectory group out of range");
+  if (hipSetDevice(c->device) != hipSuccess) return GPRX_DEVICE_ERROR;
+  // one device buffer: [gps | group | start | out]
+  const size_t o_grp = gps.size() * sizeof(gprx::RolloutGP);
+  const size_t o_st = (o_grp + (size_t)T * sizeof(int) + 15) / 16 * 16;
+  const size_t o_out = o_st + (size_t)T * 2 * nc * sizeof(double);
+  const size_t need = o_out + (size_t)T * 2 * nc * sizeof(double);
+  if (need > c->rcap) {
+    if (c->rbuf) HIPCHK(c, hipFree(c->rbuf));
+    c->rbuf = nullptr;
+    c->rcap = 0;
+    HIPCHK(c, hipMalloc(&c->rbuf, need));
+    c->rcap = need;
+  }
+  char* base = (char*)c->rbuf;
+  HIPCHK(c, hipMemcpyAsync(base, gps.data(), o_grp, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(base + o_grp, traj_group, (size_t)T * sizeof(int), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(base + o_st, start, (size_t)T * 2 * nc * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  gprx::RolloutArgs a{};
+  a.gps = (const gprx::RolloutGP*)base;
+  a.group = (const int*)(base + o_grp);
+  a.start = (const double*)(base + o_st);
+  a.out = (double*)(base + o_out);
+  a.T = T;
+  a.nc = nc;
+  a.d = dobs;
+  a.steps = steps;
+  a.usesin = usesin ? 1 : 0;
+  a.ang0 = ang0;
+  a.ang1 = ang1;
+  a.dt = dt;
+  double np = 0.0;
+  for (int t = 0; t < T; ++t)
+    for (int q = 0; q < nc; ++q) np += gps[(size_t)traj_group[t] * nc + q].N;
+  timed(c, c->stream, "rollout", np * steps * (3.0 * dobs + 24.0), np * steps * (dobs + 1) * 8.0,
+        [&] { gprx::launch_rollout(a, c->dist_mode, c->stream); });
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(final_state, base + o_out, (size_t)T * 2 * nc * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  collect(c);
+  return GPRX_OK;
+}
+
+gprx_batch* gprx_gp_batch(gprx_gp* gp) { return gp ? gp->batch : nullptr; }
 
 // ---- host CState helpers -----------------------------------------------------------------------
 int gprx_cstate_pack(int nb, const double* xc, const double* q, const double* vc, const double* wc, double* out) {

@@ -91,6 +91,26 @@ __host__ __device__ inline void op_rect(const GemmGeom& g, int nt, int mt, int& 
   }
 }
 
+// Minimal-coordinate rollout (k_rollout): one GP of a rollout group, read from a batch slot after
+// its factorisation (X: [Npad][d], alpha: Npad, params: il2[d], sf2, ...).
+struct RolloutGP {
+  const double* X;
+  const double* alpha;
+  const double* params;
+  int N;
+  int pad;
+};
+struct RolloutArgs {
+  const RolloutGP* gps;  // ngroups x nc, GP g of a group predicts the rate of coordinate g
+  const int* group;      // T: rollout group of each trajectory
+  const double* start;   // T x 2nc: (q, qdot) per coordinate (predictdynamicsmin's startobservation)
+  double* out;           // T x 2nc: (q_cur, qdot_last) per coordinate
+  int T, nc, d, steps;
+  int usesin, ang0, ang1;  // obs (sin q, cos q, qdot) for angle coordinates when usesin
+  double dt;
+};
+constexpr int ROLLOUT_DMAX = 6;
+
 // kernel launchers (gprx_kernels.hip); every launcher is asynchronous on `s`
 void launch_gram(const DevBatch& b, hipStream_t s);
 void launch_center(const DevBatch& b, hipStream_t s);
@@ -107,5 +127,6 @@ void launch_finalize(const DevBatch& b, int want_grad, hipStream_t s);
 void launch_pred_cross(const DevBatch& b, hipStream_t s);
 void launch_pred_mu(const DevBatch& b, hipStream_t s);
 void launch_pred_final(const DevBatch& b, hipStream_t s);
+void launch_rollout(const RolloutArgs& a, int dist_mode, hipStream_t s);
 
 }  // namespace gprx

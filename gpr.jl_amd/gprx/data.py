@@ -180,3 +180,53 @@ def make_trial(mech: str, N: int, M: int = 100, seed: int = 0) -> dict:
 
 def trial_seed(mech: str, trial: int) -> int:
     return 1000 * CONFIG_ID[mech] + trial
+
+
+# ---- minimal-coordinate experiments (examples/minimal_coordinates/*.jl) ---------------------
+# coordinate order of max2mincoordinates (examples/utils/data/transformations.jl:7-34):
+# per joint (q, qdot); FB uses bodies 1 and 3 (transformations.jl:25-34)
+MIN_COORDS = {"P1": (("th", "om"),), "P2": (("t1", "o1"), ("t2", "o2")), "CP": (("x", "v"), ("th", "om")),
+              "FB": (("t1", "o1"), ("t2", "o2"))}
+MIN_ANGLE = {"P1": (True,), "P2": (True, True), "CP": (False, True), "FB": (True, True)}
+
+
+def min_features(mech: str, q: np.ndarray, usesin: bool) -> np.ndarray:
+    """(n, 2nc) minimal states -> (d, n) GP inputs: per coordinate (q, qdot), or (sin q, cos q,
+    qdot) for angles when usesin (e.g. P2noise.jl(min):24-28, CPnoise.jl(min):25)."""
+    q = np.asarray(q, dtype=np.float64)
+    rows = []
+    for c, ang in enumerate(MIN_ANGLE[mech]):
+        if usesin and ang:
+            rows += [np.sin(q[:, 2 * c]), np.cos(q[:, 2 * c]), q[:, 2 * c + 1]]
+        else:
+            rows += [q[:, 2 * c], q[:, 2 * c + 1]]
+    return np.stack(rows, axis=0)
+
+
+def make_trial_min(mech: str, N: int, M: int = 100, seed: int = 0, usesin: bool = False) -> dict:
+    """One minimal-coordinate trial: X (d, N) inputs at the noisy old states, Y (nc, N) the noisy
+    next-step rates (ytrain = [[s[id] for s in xtrain_curr] for id in [2,4]], P2noise.jl(min):30),
+    start (M, 2nc) the noisy test states (xtest_old, :33)."""
+    rng = np.random.default_rng(seed)
+    m_old = _sample_minimal(mech, N, rng)
+    m_cur = _step(mech, m_old)
+    old, cur = _noisy(mech, m_old, rng), _noisy(mech, m_cur, rng)
+    keys = MIN_COORDS[mech]
+    q_old = np.stack([old[k] for pair in keys for k in pair], axis=1)
+    Y = np.stack([cur[rate] for _, rate in keys], axis=0)
+    rng_t = np.random.default_rng(seed + 500000)
+    tst = _noisy(mech, _sample_minimal(mech, M, rng_t), rng_t)
+    start = np.stack([tst[k] for pair in keys for k in pair], axis=1)
+    X = min_features(mech, q_old, usesin)
+    return dict(X=X, Y=Y, start=start, d=X.shape[0])
+
+
+def theta0_min(mech: str, key_n: int, usesin: bool = False) -> np.ndarray:
+    """θ from config '<ID>_MIN<N>' = [σ_f, ℓ per minimal coordinate]; with usesin the angle's ℓ is
+    shared by its sin and cos features (P2noise.jl(min):36)."""
+    p = np.asarray(load_theta_config()[f"{mech}_MIN{key_n}"], dtype=np.float64)
+    ell = []
+    for c, ang in enumerate(MIN_ANGLE[mech]):
+        lq, lv = p[1 + 2 * c], p[2 + 2 * c]
+        ell += [lq, lq, lv] if (usesin and ang) else [lq, lv]
+    return theta_from_params(np.concatenate([[p[0]], ell]))

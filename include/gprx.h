@@ -13,6 +13,7 @@
  *   gprx_gp_lml        update_mll! inside GP()/optimize! value evaluations   [ext] CPnoise.jl:40-41
  *   gprx_gp_lml_grad   update_mll! + update_dmll! (one LBFGS evaluation)     [ext] CPnoise.jl:41
  *   gprx_gp_predict    predict_f / predict_y(gp, x*)  examples/utils/predictdynamics.jl:13
+ *   gprx_rollout_min   predictdynamicsmin             examples/utils/predictdynamics.jl:30-102
  *   gprx_batch_*       the G per-output GPs of a trial (CPnoise.jl:37-43) and the trial loop
  *                      (examples/parallel/core.jl:28) evaluated as one device batch
  *   gprx_cstate_pack   CState(::Vector{State})      src/CState.jl:25-28
@@ -115,6 +116,27 @@ int gprx_gp_lml_grad(gprx_gp* gp, const double* theta, double* mll, double* grad
 /* f-space predictive mean (k*^T alpha) and variance (max(k** - |L^-1 k*|^2, 0)) at the
  * factorisation of the last lml call; var may be NULL.                                          */
 int gprx_gp_predict(gprx_gp* gp, const double* Xs, int M, double* mu_f, double* var_f);
+
+/* the single GP's underlying batch of one (slot 0), e.g. for gprx_rollout_min              */
+gprx_batch* gprx_gp_batch(gprx_gp* gp);
+
+/* ---- rollout in minimal coordinates (examples/utils/predictdynamics.jl:30-102) ------------ */
+#define GPRX_MECH_P1 1 /* pendulum:           q = theta                                  */
+#define GPRX_MECH_P2 2 /* double pendulum:    q = (theta1, theta2 relative)              */
+#define GPRX_MECH_CP 3 /* cart-pole:          q = (x, theta)                             */
+#define GPRX_MECH_FB 4 /* four-bar:           q = (theta1, theta3)                       */
+/* predictdynamicsmin for T trajectories in one launch.  A rollout group is the nc GPs of one
+ * trial (nc = 1 for P1, else 2; GP g predicts the rate of coordinate g), given as
+ * (batches[k], slots[k]) for k = group*nc + g, each factorised by its last gprx_batch_run with
+ * MeanZero targets.  Trajectory t uses group traj_group[t] and starts at
+ * start[t*2nc ...] = (q_1, qdot_1, ..., q_nc, qdot_nc); the GP input per step is
+ * (q, qdot) per coordinate, or (sin q, cos q, qdot) for angles when usesin (input dimension
+ * must match).  Each of the `steps` steps predicts the rates at the previous state and advances
+ * q by rate*dt, exactly as the reference loop.  final_state[t*2nc ...] = (q_cur, qdot_last);
+ * the reference's returned CState is built from q_cur with zero velocities (host side).        */
+int gprx_rollout_min(gprx_ctx* ctx, int mech, int usesin, double dt, int steps, int ngroups,
+                     gprx_batch* const* batches, const int* slots, int T, const int* traj_group,
+                     const double* start, double* final_state);
 
 /* ---- host-side CState helpers (bit-exact copies) ------------------------------------------ */
 /* out[13*b + 0..12] = [xc(3), qc.w, qc.x, qc.y, qc.z, vc(3), wc(3)] for body b (CState.jl:20,26) */

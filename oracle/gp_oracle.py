@@ -194,3 +194,46 @@ def select_outputs(Xcurr: np.ndarray, idx1) -> np.ndarray:
     (examples/maximal_coordinates/CPnoise.jl:28-29)."""
     Xcurr = np.asarray(Xcurr)
     return np.stack([Xcurr[i - 1, :] for i in idx1], axis=0)
+
+
+# ---- rollout in minimal coordinates (examples/utils/predictdynamics.jl:38-102) ---------------
+ROLL_ANGLE = {"P1": (True,), "P2": (True, True), "CP": (False, True), "FB": (True, True)}
+
+
+def rollout_min(mech: str, gps, start, steps: int, usesin: bool = False, dt: float = 0.01,
+                mode: int = DIST_EXPANDED) -> np.ndarray:
+    """predictdynamicsmin's loop for T start observations at once (each trajectory independent).
+    gps: nc tuples (X (d, N), theta, alpha) with MeanZero, GP g predicting coordinate g's rate.
+    start: (T, 2nc) = (q_old, qdot_old) per coordinate.  Returns (T, 2nc) = (q_curr, qdot_last).
+
+      qcurr = qold + Δt*qdot_old                                 (:41, :55, :72, :87)
+      for 1:steps
+          obs = (q_old, qdot_old) or (sin, cos, qdot) per angle   (:43, :57, :74, :89)
+          qdot_curr_g = predict_y(gp_g, obs)[1][1]               (:44, :58, :75, :90)
+          q_old, qdot_old = q_curr, qdot_curr ; q_curr += qdot_curr*Δt   (:45-46, :59-61, ...)
+    """
+    ang = ROLL_ANGLE[mech]
+    nc = len(ang)
+    st = np.array(start, dtype=np.float64).reshape(-1, 2 * nc)
+    qo = st[:, 0::2].copy()
+    vo = st[:, 1::2].copy()
+    qc = qo + dt * vo
+    for _ in range(steps):
+        rows = []
+        for c in range(nc):
+            if usesin and ang[c]:
+                rows += [np.sin(qo[:, c]), np.cos(qo[:, c]), vo[:, c]]
+            else:
+                rows += [qo[:, c], vo[:, c]]
+        obs = np.stack(rows, axis=0)  # (d, T)
+        pred = np.empty_like(qo)
+        for g, (X, theta, alpha) in enumerate(gps):
+            il2, sf2, _, _ = kernel_params(np.asarray(theta, dtype=np.float64), X.shape[0])
+            Ks = sf2 * np.exp(-weighted_r(dist_stack(np.asarray(X, dtype=np.float64), obs, mode), il2) * 0.5)
+            pred[:, g] = Ks.T @ alpha
+        qo, vo = qc.copy(), pred
+        qc = qc + pred * dt
+    out = np.empty_like(st)
+    out[:, 0::2] = qc
+    out[:, 1::2] = vo
+    return out
