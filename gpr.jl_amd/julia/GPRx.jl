@@ -104,4 +104,26 @@ function GaussianProcesses.predict_f(gp::GPE{<:Any,<:Any,<:Mean,<:SEArd}, x::Abs
     return mu .+ GaussianProcesses.mean(gp.mean, xs), var   # predict_y adds exp(2 logNoise)
 end
 
+# predictdynamicsmin (examples/utils/predictdynamics.jl:30-102) for all test observations of one
+# trial in one device launch.  `gps` must be MeanZero GPEs evaluated on this thread's context (the
+# experiment's own thread, core.jl:28).  Returns the (q_cur, q̇_last) per coordinate and
+# trajectory; the caller builds the CState from q_cur as predictdynamics.jl:48-101 does.
+const MECH = Dict("P1" => Cint(1), "P2" => Cint(2), "CP" => Cint(3), "FB" => Cint(4))
+function rollout_min(etype::String, gps::Vector{<:GPE}, startobservations::Vector{Vector{Float64}},
+                     steps::Integer; usesin::Bool=false, Δt::Real=0.01)
+    haskey(MECH, etype) || throw(ArgumentError("Experiment $etype not supported!"))
+    all(gp -> gp.mean isa MeanZero, gps) || error("gprx: device rollouts need MeanZero GPs")
+    T = length(startobservations)
+    nc = etype == "P1" ? 1 : 2
+    fin = zeros(2nc, T)
+    bs = [ccall((:gprx_gp_batch, LIB), Ptr{Cvoid}, (Ptr{Cvoid},), handle(gp).ptr) for gp in gps]
+    rc = ccall((:gprx_rollout_min, LIB), Cint,
+               (Ptr{Cvoid}, Cint, Cint, Cdouble, Cint, Cint, Ptr{Ptr{Cvoid}}, Ptr{Cint}, Cint, Ptr{Cint},
+                Ptr{Float64}, Ptr{Float64}),
+               context(), MECH[etype], Cint(usesin), Float64(Δt), Cint(steps), Cint(1), bs, zeros(Cint, nc),
+               Cint(T), zeros(Cint, T), reduce(hcat, startobservations), fin)
+    check(rc, gps)
+    return [fin[:, t] for t in 1:T]
+end
+
 end # module
