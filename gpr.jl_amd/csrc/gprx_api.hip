@@ -37,7 +37,7 @@ struct gprx_ctx {
   hipStream_t stream = nullptr;
   std::mutex mu;
   std::string err;
-  int dist_mode = GPRX_DIST_EXPANDED;
+  int dist_mode = GPRX_DIST_DIRECT;  // the Gram of GaussianProcesses cov_ij (distij) [ext]
   bool prof = false;
   std::map<std::string, KStat> stats;
   std::vector<hipEvent_t> evpool;

@@ -90,6 +90,14 @@ __device__ __forceinline__ double sqd(double a, double b, int mode) {
   return t * t;
 }
 // same with the squares precomputed
+// r + d(a, b) w with the oracle's rounding (no contraction: a fused accumulation moves the LML of
+// the ill-conditioned cartpole cases by ~1e-9 relative, beyond the parity bound).  Direct mode is
+// distij's s += (a-b)^2 w: 4 fp64 ops per element and dimension, expanded 6.
+__device__ __forceinline__ double sqd2(double a, double a2, double b, double b2, int mode);
+template <int MODE>
+__device__ __forceinline__ double wacc(double r, double a, double a2, double b, double b2, double w) {
+  return r + sqd2(a, a2, b, b2, MODE) * w;
+}
 __device__ __forceinline__ double sqd2(double a, double a2, double b, double b2, int mode) {
   if (mode == 0) {
     const double v = fma(-2.0, a * b, a2 + b2);
@@ -437,7 +445,7 @@ __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
-      for (int b = 0; b < 4; ++b) rr[a][b] = rr[a][b] + sqd2(av[a], a2[a], bv[b], b2[b], MODE) * w;
+      for (int b = 0; b < 4; ++b) rr[a][b] = wacc<MODE>(rr[a][b], av[a], a2[a], bv[b], b2[b], w);
   }
   double* K = db.K + (size_t)slot * db.mat;
 #pragma unroll
@@ -1774,7 +1782,7 @@ __global__ __launch_bounds__(NTHR) void k_pred_cross(DevBatch db) {
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
-      for (int b = 0; b < 4; ++b) rr[a][b] = rr[a][b] + sqd2(av[a], a2[a], bv[b], b2[b], MODE) * wgt;
+      for (int b = 0; b < 4; ++b) rr[a][b] = wacc<MODE>(rr[a][b], av[a], a2[a], bv[b], b2[b], wgt);
   }
   double* KsT = db.KsT + (size_t)slot * db.Npad * db.Mpad;
 #pragma unroll
@@ -1900,7 +1908,7 @@ __global__ __launch_bounds__(NT) void k_rollout(RolloutArgs a) {
           double r = 0.0;
 #pragma unroll
           for (int p = 0; p < 6; ++p)
-            if (p < d) r = r + sqd2(xv[u][p], xv[u][p] * xv[u][p], ov[p], ov2[p], MODE) * il2[p];
+            if (p < d) r = wacc<MODE>(r, xv[u][p], xv[u][p] * xv[u][p], ov[p], ov2[p], il2[p]);
           if (j0 + u * NT < G.N) s = fma(sf2 * exp(-r * 0.5), al[u], s);
         }
       }

@@ -34,7 +34,7 @@ def _release_all():
 class Context:
     """One device + one HIP stream (gprx_ctx).  Safe to share across threads; calls serialise."""
 
-    def __init__(self, device: int = 0, dist_mode: int = L.DIST_EXPANDED):
+    def __init__(self, device: int = 0, dist_mode: int = L.DIST_DIRECT):
         h = C.c_void_p()
         L.check(L.lib.gprx_ctx_create(int(device), C.byref(h)))
         self.h = h

@@ -55,8 +55,13 @@ extern "C" {
 #define GPRX_WANT_PREDICT 2u /* predictive mean + variance at the batch's test points    */
 
 /* squared-distance formulation of the SE-ARD kernel (see DESIGN.md "distance modes") */
-#define GPRX_DIST_EXPANDED 0 /* Distances.jl 0.10.5 pairwise SqEuclidean: a^2 + b^2 - 2ab (default) */
-#define GPRX_DIST_DIRECT 1   /* (a - b)^2                                                            */
+/* Per-dimension squared distance in the Gram / cross-covariance:
+ *   DIRECT   (default): sum_d w_d (a_d - b_d)^2, as GaussianProcesses' cov_ij for StationaryARD
+ *            kernels (distij over WeightedSqEuclidean) [ext]
+ *   EXPANDED: a^2 + b^2 - 2ab clamped at 0 per dimension, the rounding of the Distances.jl 0.10.5
+ *            pairwise(SqEuclidean()) stack that GaussianProcesses keeps for gradients [ext]       */
+#define GPRX_DIST_EXPANDED 0
+#define GPRX_DIST_DIRECT 1
 
 /* memory kind of pointer arguments */
 #define GPRX_MEM_HOST 0

@@ -33,6 +33,12 @@ EPS = float(np.finfo(np.float64).eps)  # Julia's eps()
 
 DIST_EXPANDED = 0
 DIST_DIRECT = 1
+# [ext] GaussianProcesses' cov_ij for StationaryARD kernels evaluates the Gram (and the predictive
+# cross-covariance) through distij over WeightedSqEuclidean: s += w_d (x1_d - x2_d)^2 -- exact
+# differences, the DIST_DIRECT form and the default here.  The per-dimension Distances.jl stack
+# (DIST_EXPANDED rounding) is kept by KernelData for the gradient; restating the whole path in that
+# rounding is the second formulation whose spread calibrates the tolerances.
+DEFAULT_MODE = DIST_DIRECT
 
 
 def kernel_params(theta: np.ndarray, d: int):
@@ -50,13 +56,13 @@ def kernel_params(theta: np.ndarray, d: int):
     return il2, sf2, sn2, sn2 + EPS
 
 
-def dist_stack(XA: np.ndarray, XB: np.ndarray, mode: int = DIST_EXPANDED) -> np.ndarray:
+def dist_stack(XA: np.ndarray, XB: np.ndarray, mode: int = DIST_DIRECT) -> np.ndarray:
     """Per-dimension squared distances, shape (d, NA, NB).
 
     [ext] GaussianProcesses' KernelData for StationaryARD kernels fills dist_stack[:,:,p] with
     Distances.jl 0.10.5 pairwise(SqEuclidean(), X1[p:p,:], X2[p:p,:]), whose _pairwise! expands
     |a-b|^2 = a^2 + b^2 - 2ab (clamped at 0)  -> mode DIST_EXPANDED.
-    DIST_DIRECT is the exact-difference form (a-b)^2.
+    DIST_DIRECT is the exact-difference form (a-b)^2 of cov_ij / distij (the default).
     """
     A = np.asarray(XA, dtype=np.float64)
     B = np.asarray(XB, dtype=np.float64)
@@ -78,7 +84,7 @@ def weighted_r(D: np.ndarray, il2: np.ndarray) -> np.ndarray:
     return r
 
 
-def gram(X: np.ndarray, theta: np.ndarray, mode: int = DIST_EXPANDED, D: np.ndarray | None = None):
+def gram(X: np.ndarray, theta: np.ndarray, mode: int = DIST_DIRECT, D: np.ndarray | None = None):
     """[ext] update_cK!: K = σ2 exp(-r/2) + (exp(2 logNoise) + eps) I, plus the noise-free Kf."""
     d = X.shape[0]
     il2, sf2, sn2, noise = kernel_params(theta, d)
@@ -110,7 +116,7 @@ def cholesky_upper(K: np.ndarray) -> np.ndarray:
     return U
 
 
-def lml(X, y, theta, mode: int = DIST_EXPANDED, want_grad: bool = False, D=None):
+def lml(X, y, theta, mode: int = DIST_DIRECT, want_grad: bool = False, D=None):
     """update_mll! (+ update_dmll!) restated [ext].
 
     mll  = -(y'α + logdet(K) + N log2π)/2,  α = K \\ y,  logdet = 2 Σ log U_ii
@@ -144,7 +150,7 @@ def lml(X, y, theta, mode: int = DIST_EXPANDED, want_grad: bool = False, D=None)
     return mll, g, aux
 
 
-def predict_f(X, theta, alpha, U, Xs, mode: int = DIST_EXPANDED):
+def predict_f(X, theta, alpha, U, Xs, mode: int = DIST_DIRECT):
     """[ext] predict_f(gp, x*; full_cov=false): per test point k* = σ2 exp(-r(X, x*)/2),
     μ = k*'α, v = U'⁻¹ k* (whiten!), σ² = max(Kpred - v'v, 0), Kpred = σ2 exp(-r(x*,x*)/2)."""
     X = np.asarray(X, dtype=np.float64)
@@ -159,7 +165,7 @@ def predict_f(X, theta, alpha, U, Xs, mode: int = DIST_EXPANDED):
     return mu, var
 
 
-def predict_y(X, theta, alpha, U, Xs, mean_s=None, mode: int = DIST_EXPANDED):
+def predict_y(X, theta, alpha, U, Xs, mean_s=None, mode: int = DIST_DIRECT):
     """[ext] predict_y = predict_f + prior mean, variance + exp(2 logNoise)."""
     mu, var = predict_f(X, theta, alpha, U, Xs, mode)
     if mean_s is not None:
@@ -167,10 +173,14 @@ def predict_y(X, theta, alpha, U, Xs, mean_s=None, mode: int = DIST_EXPANDED):
     return mu, var + math.exp(2.0 * float(theta[0]))
 
 
-def fit(X, y, theta, Xs=None, mode: int = DIST_EXPANDED):
-    """One 'fit' (SURVEY.md section 8d): Gram+Cholesky+α+LML, ∂LML, predict at Xs."""
+def fit(X, y, theta, Xs=None, mode: int = DIST_DIRECT):
+    """One 'fit' (SURVEY.md section 8d): Gram+Cholesky+α+LML, ∂LML, predict at Xs.
+
+    mll_sens (test calibration, not part of the reference's output): 4 eps ||W o K||_F, the size of
+    the LML change under a random 4-ulp relative perturbation of K (dLML = ½ Σ W_ij dK_ij) -- what
+    any other summation order of the Gram or of a blocked factorisation can move the LML by."""
     m, g, aux = lml(X, y, theta, mode, want_grad=True)
-    out = dict(mll=m, grad=g, alpha=aux["alpha"])
+    out = dict(mll=m, grad=g, alpha=aux["alpha"], mll_sens=4.0 * EPS * float(np.linalg.norm(aux["W"] * aux["K"])))
     if Xs is not None:
         mu, var = predict_f(X, theta, aux["alpha"], aux["U"], Xs, mode)
         out["mu"] = mu
@@ -201,7 +211,7 @@ ROLL_ANGLE = {"P1": (True,), "P2": (True, True), "CP": (False, True), "FB": (Tru
 
 
 def rollout_min(mech: str, gps, start, steps: int, usesin: bool = False, dt: float = 0.01,
-                mode: int = DIST_EXPANDED) -> np.ndarray:
+                mode: int = DIST_DIRECT) -> np.ndarray:
     """predictdynamicsmin's loop for T start observations at once (each trajectory independent).
     gps: nc tuples (X (d, N), theta, alpha) with MeanZero, GP g predicting coordinate g's rate.
     start: (T, 2nc) = (q_old, qdot_old) per coordinate.  Returns (T, 2nc) = (q_curr, qdot_last).
