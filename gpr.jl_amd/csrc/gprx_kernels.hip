@@ -272,23 +272,27 @@ constexpr int QM = 4, QN = 4;
 struct Frag4 {
   double a[4][QM], b[4][QN];
 };
+// NB < QN: only the first NB 16-column blocks of B (the prediction's last, partly padded test tile)
+template <int NB = QN>
 __device__ __forceinline__ void frag4_load(Frag4& f, const double* pa, const double* pb, size_t sa, size_t sb) {
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
 #pragma unroll
     for (int a = 0; a < QM; ++a) f.a[s][a] = pa[s * sa + 16 * a];
 #pragma unroll
-    for (int b = 0; b < QN; ++b) f.b[s][b] = pb[s * sb + 16 * b];
+    for (int b = 0; b < NB; ++b) f.b[s][b] = pb[s * sb + 16 * b];
   }
 }
+template <int NB = QN>
 __device__ __forceinline__ void frag4_mma(d4 (&acc)[QM][QN], const Frag4& f) {
 #pragma unroll
   for (int s = 0; s < 4; ++s)
 #pragma unroll
     for (int a = 0; a < QM; ++a)
 #pragma unroll
-      for (int b = 0; b < QN; ++b) acc[a][b] = mfma(f.b[s][b], f.a[s][a], acc[a][b]);
+      for (int b = 0; b < NB; ++b) acc[a][b] = mfma(f.b[s][b], f.a[s][a], acc[a][b]);
 }
+template <int NB = QN>
 __device__ __forceinline__ void mma_64x64(d4 (&acc)[QM][QN], const double* __restrict__ A, size_t lda,
                                           const double* __restrict__ B, size_t ldb, int K) {
   const int nst = __builtin_amdgcn_readfirstlane(K >> 4);  // even: K is whole 64-tiles
@@ -298,13 +302,13 @@ __device__ __forceinline__ void mma_64x64(d4 (&acc)[QM][QN], const double* __res
   const double* pb = B + lr + (size_t)lk * ldb;
   const size_t sa = 4 * lda, sb = 4 * ldb;
   Frag4 f0, f1;
-  frag4_load(f0, pa, pb, sa, sb);
+  frag4_load<NB>(f0, pa, pb, sa, sb);
   for (int it = 0; it < nst; it += 2) {
-    frag4_load(f1, pa + (size_t)(it + 1) * 4 * sa, pb + (size_t)(it + 1) * 4 * sb, sa, sb);
-    frag4_mma(acc, f0);
+    frag4_load<NB>(f1, pa + (size_t)(it + 1) * 4 * sa, pb + (size_t)(it + 1) * 4 * sb, sa, sb);
+    frag4_mma<NB>(acc, f0);
     const int n2 = (it + 2 < nst) ? it + 2 : nst - 1;
-    frag4_load(f0, pa + (size_t)n2 * 4 * sa, pb + (size_t)n2 * 4 * sb, sa, sb);
-    frag4_mma(acc, f1);
+    frag4_load<NB>(f0, pa + (size_t)n2 * 4 * sa, pb + (size_t)n2 * 4 * sb, sa, sb);
+    frag4_mma<NB>(acc, f1);
   }
 }
 __device__ __forceinline__ void acc4_zero(d4 (&acc)[QM][QN]) {
@@ -943,8 +947,9 @@ __global__ __launch_bounds__(64) void k_diag_w(DevBatch db, int jt) {
 // return at once (no workgroup barrier in this kernel).
 // ============================================================================================
 // One 64 x 64 output tile (ti, tj) of a GemmOp on one wave.
+template <bool PV>
 __device__ __forceinline__ void gemm_tile(const DevBatch& db, const GemmGeom& g, int slot, int ti, int tj) {
-  const int op = g.op;
+  const int op = PV ? (int)OP_PREDVAR : g.op;
   const size_t ld = db.ld, so = (size_t)slot * db.mat;
   int kb, ke;  // K range in tiles
   const double *A, *Bm;
@@ -975,8 +980,18 @@ __device__ __forceinline__ void gemm_tile(const DevBatch& db, const GemmGeom& g,
   } else {
     acc4_zero(acc);
   }
-  mma_64x64(acc, A + (size_t)kb * TS * ld + ti * TS, ld, Bm + (size_t)kb * TS * ldb + tj * TS, ldb, (ke - kb) * TS);
-  if (op == OP_PREDVAR) {
+  const double* Ak = A + (size_t)kb * TS * ld + ti * TS;
+  const double* Bk = Bm + (size_t)kb * TS * ldb + tj * TS;
+  if constexpr (PV) {  // prediction (own kernel instance): skip the last test tile's all-padding blocks
+    const int nbv = __builtin_amdgcn_readfirstlane((db.M - tj * TS + 15) >> 4);
+    if (nbv >= QN) mma_64x64(acc, Ak, ld, Bk, ldb, (ke - kb) * TS);
+    else if (nbv == 3) mma_64x64<3>(acc, Ak, ld, Bk, ldb, (ke - kb) * TS);
+    else if (nbv == 2) mma_64x64<2>(acc, Ak, ld, Bk, ldb, (ke - kb) * TS);
+    else mma_64x64<1>(acc, Ak, ld, Bk, ldb, (ke - kb) * TS);
+  } else {
+    mma_64x64(acc, Ak, ld, Bk, ldb, (ke - kb) * TS);
+  }
+  if (PV) {  // OP_PREDVAR runs only in the k_gemm_pv instance
 #pragma unroll
     for (int b = 0; b < QN; ++b)
 #pragma unroll
@@ -1030,6 +1045,7 @@ __device__ __forceinline__ void gemm_tile(const DevBatch& db, const GemmGeom& g,
   }
 }
 
+template <bool PV>
 __device__ __forceinline__ void gemm_body(const DevBatch& db, const GemmGeom& g1, const GemmGeom& g2) {
   int r0, c0, R, C, r02, c02, R2, C2;
   bool tri, tri2;
@@ -1078,7 +1094,7 @@ __device__ __forceinline__ void gemm_body(const DevBatch& db, const GemmGeom& g1
     if (ur + wr >= R || uc + wc >= C) continue;  // wave-uniform: partial unit
     if (tri && uc + wc > ur + wr) continue;      // above the diagonal
     // wave-uniform tile indices in SGPRs (the 64 x 64 core needs every VGPR)
-    gemm_tile(db, g, slot, __builtin_amdgcn_readfirstlane(r0 + ur + wr), __builtin_amdgcn_readfirstlane(c0 + uc + wc));
+    gemm_tile<PV>(db, g, slot, __builtin_amdgcn_readfirstlane(r0 + ur + wr), __builtin_amdgcn_readfirstlane(c0 + uc + wc));
   }
 }
 
@@ -1237,7 +1253,10 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4))) vo
   gemm_body_pair(db, g, g2);
 }
 __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_gemm(DevBatch db, GemmGeom g, GemmGeom g2) {
-  gemm_body(db, g, g2);
+  gemm_body<false>(db, g, g2);
+}
+__global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_gemm_pv(DevBatch db, GemmGeom g, GemmGeom g2) {
+  gemm_body<true>(db, g, g2);
 }
 
 // ============================================================================================
@@ -1986,7 +2005,8 @@ void launch_gemm(const DevBatch& b, const GemmGeom& g, hipStream_t s, const Gemm
   int T = op_units(g, b.nt, b.mt);
   if (g2.op != OP_NONE) T += op_units(g2, b.nt, b.mt);
   const size_t lds = (g.op == OP_LINV21 || g2.op == OP_LINV21) ? 4 * 16 * (TS + 1) * sizeof(double) : 0;
-  hipLaunchKernelGGL(k_gemm, dim3(grid_blocks(b.B, T)), dim3(NTHR), lds, s, b, g, g2);
+  if (g.op == OP_PREDVAR) hipLaunchKernelGGL(k_gemm_pv, dim3(grid_blocks(b.B, T)), dim3(NTHR), lds, s, b, g, g2);
+  else hipLaunchKernelGGL(k_gemm, dim3(grid_blocks(b.B, T)), dim3(NTHR), lds, s, b, g, g2);
 }
 void launch_alpha(const DevBatch& b, hipStream_t s, int phase) {
   hipLaunchKernelGGL(k_alpha, dim3(grid_blocks(b.B, b.nt)), dim3(NTHR), 0, s, b, phase);
