@@ -90,13 +90,15 @@ __device__ __forceinline__ double sqd(double a, double b, int mode) {
   return t * t;
 }
 // same with the squares precomputed
-// r + d(a, b) w with the oracle's rounding (no contraction: a fused accumulation moves the LML of
-// the ill-conditioned cartpole cases by ~1e-9 relative, beyond the parity bound).  Direct mode is
-// distij's s += (a-b)^2 w: 4 fp64 ops per element and dimension, expanded 6.
+// r + d(a, b) w.  Expanded mode keeps the Distances.jl stack's rounding (d, then w d, then +; 6 fp64
+// ops per element and dimension).  Direct mode is distij's s += (a-b)^2 w with the accumulation
+// fused (3 ops): a rounding-level reordering, like the reference's own @simd sum.
 __device__ __forceinline__ double sqd2(double a, double a2, double b, double b2, int mode);
 template <int MODE>
 __device__ __forceinline__ double wacc(double r, double a, double a2, double b, double b2, double w) {
-  return r + sqd2(a, a2, b, b2, MODE) * w;
+  if (MODE == 0) return r + sqd2(a, a2, b, b2, 0) * w;
+  const double t = a - b;
+  return __builtin_fma(t * t, w, r);
 }
 __device__ __forceinline__ double sqd2(double a, double a2, double b, double b2, int mode) {
   if (mode == 0) {
