@@ -92,7 +92,8 @@ __device__ __forceinline__ double sqd(double a, double b, int mode) {
 // same with the squares precomputed
 // r + d(a, b) w.  Expanded mode keeps the Distances.jl stack's rounding (d, then w d, then +; 6 fp64
 // ops per element and dimension).  Direct mode is distij's s += (a-b)^2 w with the accumulation
-// fused (3 ops): a rounding-level reordering, like the reference's own @simd sum.
+// fused (3 ops): a rounding-level reordering, like the reference's own @simd sum.  (k_gram and
+// k_pred_cross go one step further in direct mode: coordinates pre-scaled by 1/ell, 2 ops.)
 __device__ __forceinline__ double sqd2(double a, double a2, double b, double b2, int mode);
 template <int MODE>
 __device__ __forceinline__ double wacc(double r, double a, double a2, double b, double b2, double w) {
@@ -419,12 +420,18 @@ __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
     i = c + u;
   }
   const double* X = db.X + (size_t)slot * db.Npad * d;
+  const double* P = db.params + (size_t)slot * db.pst;
+  double* sc = pw + DMAX + 4;  // direct mode: coordinates pre-scaled by 1/ell_p = sqrt(il2_p)
+  if (MODE == 1) {
+    for (int e = tid; e < d; e += NTHR) sc[e] = sqrt(P[e]);
+    __syncthreads();
+  }
   for (int e = tid; e < TS * d; e += NTHR) {
     const int r = e / d, p = e - r * d;
-    xi[p * TS + r] = X[(size_t)i * TS * d + e];
-    xj[p * TS + r] = X[(size_t)j * TS * d + e];
+    const double s = MODE == 1 ? sc[p] : 1.0;
+    xi[p * TS + r] = X[(size_t)i * TS * d + e] * s;
+    xj[p * TS + r] = X[(size_t)j * TS * d + e] * s;
   }
-  const double* P = db.params + (size_t)slot * db.pst;
   for (int e = tid; e < d + 3; e += NTHR) pw[e] = P[e];
   __syncthreads();
   const double sf2 = pw[d], noise = pw[d + 1];
@@ -451,7 +458,14 @@ __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
-      for (int b = 0; b < 4; ++b) rr[a][b] = wacc<MODE>(rr[a][b], av[a], a2[a], bv[b], b2[b], w);
+      for (int b = 0; b < 4; ++b) {
+        if (MODE == 0) {
+          rr[a][b] = wacc<0>(rr[a][b], av[a], a2[a], bv[b], b2[b], w);
+        } else {  // r += (a/ell - b/ell)^2: 2 fp64 ops per element and dimension
+          const double t = av[a] - bv[b];
+          rr[a][b] = __builtin_fma(t, t, rr[a][b]);
+        }
+      }
   }
   double* K = db.K + (size_t)slot * db.mat;
 #pragma unroll
@@ -1770,12 +1784,18 @@ __global__ __launch_bounds__(NTHR) void k_pred_cross(DevBatch db) {
   const int ch = t / db.mt, mtile = t - ch * db.mt;
   const double* X = db.X + (size_t)slot * db.Npad * d;
   const double* Xq = db.Xs + (size_t)slot * db.Mpad * d;
+  const double* P = db.params + (size_t)slot * db.pst;
+  double* sc = pw + DMAX + 4;  // as k_gram
+  if (MODE == 1) {
+    for (int e = tid; e < d; e += NTHR) sc[e] = sqrt(P[e]);
+    __syncthreads();
+  }
   for (int e = tid; e < TS * d; e += NTHR) {
     const int r = e / d, p = e - r * d;
-    xt[p * TS + r] = X[(size_t)ch * TS * d + e];
-    xs[p * TS + r] = Xq[(size_t)mtile * TS * d + e];
+    const double s = MODE == 1 ? sc[p] : 1.0;
+    xt[p * TS + r] = X[(size_t)ch * TS * d + e] * s;
+    xs[p * TS + r] = Xq[(size_t)mtile * TS * d + e] * s;
   }
-  const double* P = db.params + (size_t)slot * db.pst;
   for (int e = tid; e < d + 3; e += NTHR) pw[e] = P[e];
   __syncthreads();
   const double sf2 = pw[d];
@@ -1803,7 +1823,14 @@ __global__ __launch_bounds__(NTHR) void k_pred_cross(DevBatch db) {
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
-      for (int b = 0; b < 4; ++b) rr[a][b] = wacc<MODE>(rr[a][b], av[a], a2[a], bv[b], b2[b], wgt);
+      for (int b = 0; b < 4; ++b) {
+        if (MODE == 0) {
+          rr[a][b] = wacc<0>(rr[a][b], av[a], a2[a], bv[b], b2[b], wgt);
+        } else {  // as k_gram
+          const double t = av[a] - bv[b];
+          rr[a][b] = __builtin_fma(t, t, rr[a][b]);
+        }
+      }
   }
   double* KsT = db.KsT + (size_t)slot * db.Npad * db.Mpad;
 #pragma unroll
@@ -1966,11 +1993,11 @@ __global__ __launch_bounds__(NT) void k_rollout(RolloutArgs a) {
 // ---------------------------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------------------------
-static size_t gram_lds(int d) { return (size_t)(2 * d * TS + DMAX + 4) * sizeof(double); }
+static size_t gram_lds(int d) { return (size_t)(2 * d * TS + 2 * DMAX + 4) * sizeof(double); }
 static size_t lauum_lds(int d) {
   return (size_t)(4 * (16 * ((d + 15) / 16) + 1) * TS + 4 * SPW + 8 * TS + DMAX) * sizeof(double);
 }
-static size_t cross_lds(int d) { return (size_t)(2 * d * TS + DMAX + 4) * sizeof(double); }
+static size_t cross_lds(int d) { return (size_t)(2 * d * TS + 2 * DMAX + 4) * sizeof(double); }
 
 static void set_lds_limits() {
   static bool done = false;
