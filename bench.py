@@ -112,7 +112,7 @@ def cpu_baseline(X, Y, T, XT, gpu=None, max_seconds: float = 15.0, max_fits: int
     dt = time.perf_counter() - t0
     base = dict(value=n / dt, unit="fits/s", cores=int(threads), kind="port",
                 sample=f"{n} P2 fits (N=2048, d=26, M=100) via oracle/gp_oracle.py: reference algorithm "
-                       f"(Distances-style dist stack, OpenBLAS dpotrf, K^-1 by cho_solve(I), per-param grad "
+                       f"(distij direct distances, OpenBLAS dpotrf, K^-1 by cho_solve(I), per-param grad "
                        f"sums), {dt:.1f}s, OpenBLAS threads={threads}")
     acc = None
     if gpu is not None:
