@@ -76,6 +76,24 @@ def dist_stack(XA: np.ndarray, XB: np.ndarray, mode: int = DIST_DIRECT) -> np.nd
     return t * t
 
 
+def dist_lazy(XA: np.ndarray, XB: np.ndarray, mode: int = DIST_DIRECT):
+    """The same stack as dist_stack, one dimension at a time (a list-like of (NA, NB) arrays made
+    on access): the large configurations (FB N=4096, d=52: a 7 GB stack) keep one slice alive."""
+    A = np.asarray(XA, dtype=np.float64)
+    B = np.asarray(XB, dtype=np.float64)
+
+    class _Lazy:
+        shape = (A.shape[0], A.shape[1], B.shape[1])
+
+        def __getitem__(self, p):
+            return dist_stack(A[p:p + 1], B[p:p + 1], mode)[0]
+
+    return _Lazy()
+
+
+STACK_MAX = 1 << 28  # elements; above this the stack is evaluated lazily (identical arithmetic)
+
+
 def weighted_r(D: np.ndarray, il2: np.ndarray) -> np.ndarray:
     """r_ij = sum_p D[p,i,j] * iℓ2_p, accumulated in order p = 1..d from 0.0 (cov_ij loop)."""
     r = np.zeros(D.shape[1:], dtype=np.float64)
@@ -89,7 +107,7 @@ def gram(X: np.ndarray, theta: np.ndarray, mode: int = DIST_DIRECT, D: np.ndarra
     d = X.shape[0]
     il2, sf2, sn2, noise = kernel_params(theta, d)
     if D is None:
-        D = dist_stack(X, X, mode)
+        D = dist_stack(X, X, mode) if d * X.shape[1] ** 2 <= STACK_MAX else dist_lazy(X, X, mode)
     Kf = sf2 * np.exp(-weighted_r(D, il2) * 0.5)
     K = Kf.copy()
     idx = np.arange(K.shape[0])

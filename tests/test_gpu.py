@@ -358,3 +358,52 @@ def test_mean_only_prediction_matches_full(gprx, ctx, golden_dir):
     gp = gprx.GP(X, Y[1], gprx.MeanZero(), gprx.SEArd(th[1:-1], th[-1]), ctx=ctx)
     m_full, _ = gp.predict_y(Xs)
     np.testing.assert_array_equal(gp.predict_y_mean(Xs), m_full)
+
+
+def test_fb_full_size_n4096_d52(gprx, ctx):
+    """BASELINE config FB: N=4096, d=52, the 12 per-output GPs of one trial with a theta-independent
+    prior mean subtracted (MeanDynamics role), M=100 test states.  Two slots against the oracle
+    (mll, gradient, mean, variance; the LML bound uses the oracle's rounding sensitivity), every
+    slot finite and bit-identical across repeated runs."""
+    from gprx import data
+
+    tr = data.make_trial("FB", 4096, 100, seed=data.trial_seed("FB", 0))
+    th = data.theta0("FB", 512)  # the largest FB key of config.json
+    G = tr["Y"].shape[0]
+    mu0 = 0.05 * tr["X"][8]  # a theta-independent prior mean over the training states
+    Y = tr["Y"] - mu0
+    b = gprx.GPBatch(G, 52, 4096, 100, ctx=ctx)
+    b.set_train(tr["X"], Y)
+    b.set_test(tr["Xs"])
+    T = np.tile(th, (G, 1))
+    r1 = b.run(T, grad=True, predict=True)
+    r2 = b.run(T, grad=True, predict=True)
+    assert np.all(r1["status"] == 0)
+    for k in ("mll", "grad", "mu", "var"):
+        assert np.all(np.isfinite(r1[k]))
+        np.testing.assert_array_equal(r1[k], r2[k])
+    for s in (0, 7):
+        f = O.fit(tr["X"], Y[s], th, tr["Xs"], ctx.dist_mode)
+        assert abs(r1["mll"][s] - f["mll"]) <= max(TOL_MLL * abs(f["mll"]), 10 * f["mll_sens"])
+        assert np.max(np.abs(r1["grad"][s] - f["grad"])) <= TOL_GRAD * max(1.0, np.max(np.abs(f["grad"])))
+        assert np.max(np.abs(r1["mu"][s] - f["mu"])) <= TOL_MU * np.max(np.abs(Y[s]))
+        assert np.max(np.abs(r1["var"][s] - f["var"])) <= TOL_VAR * math.exp(2 * th[-1])
+    b.close()
+
+
+def test_cp_all_26_outputs_n512(gprx, ctx):
+    """BASELINE config CP: N=512, d=26, all 26 CState coordinates as output GPs of one trial (one
+    batch sharing X); three outputs against the oracle in both distance tolerances."""
+    from gprx import data
+
+    tr = data.make_trial("CP", 512, 64, seed=data.trial_seed("CP", 3))
+    Y = tr["Xcurr"]  # 26 x N: every coordinate of the next state
+    th = data.theta0("CP", 512)
+    b = gprx.GPBatch(26, 26, 512, 64, ctx=ctx)
+    b.set_train(tr["X"], Y)
+    b.set_test(tr["Xs"])
+    r = b.run(np.tile(th, (26, 1)), grad=True, predict=True)
+    assert np.all(r["status"] == 0)  # one K for all outputs; constant coordinates just give y = 0
+    for s in (0, 8, 21, 22):  # a constant coordinate, cart v_y, pole omega_x, pole v_y
+        check_slot(r, s, tr["X"], Y[s], th, tr["Xs"], ctx.dist_mode)
+    b.close()
