@@ -98,9 +98,11 @@ int set_err(gprx_ctx* c, int code, const std::string& msg) {
 #define HIPCHK(ctx, expr)                                                                          \
   do {                                                                                             \
     hipError_t e_ = (expr);                                                                        \
-    if (e_ != hipSuccess)                                                                          \
+    if (e_ != hipSuccess) {                                                                        \
+      (void)hipGetLastError(); /* not sticky for the context's next call */                        \
       return set_err((ctx), e_ == hipErrorOutOfMemory ? GPRX_OUT_OF_MEMORY : GPRX_DEVICE_ERROR,     \
                      std::string(#expr) + ": " + hipGetErrorString(e_));                           \
+    }                                                                                              \
   } while (0)
 
 hipEvent_t ev_get(gprx_ctx* c) {
@@ -190,6 +192,7 @@ int dalloc(gprx_batch* b, T** p, size_t count) {
   if (count == 0) count = 1;
   hipError_t e = hipMalloc(&q, count * sizeof(T));
   if (e != hipSuccess) {
+    (void)hipGetLastError();  // clear the runtime's sticky error: later calls check hipGetLastError
     *p = nullptr;
     return set_err(b->ctx, e == hipErrorOutOfMemory ? GPRX_OUT_OF_MEMORY : GPRX_DEVICE_ERROR,
                    std::string("hipMalloc: ") + hipGetErrorString(e));
@@ -215,8 +218,11 @@ int alloc_test(gprx_batch* b, int M_max) {
   if ((rc = dalloc(b, &db.var_part, B * db.nt * (size_t)db.Mpad))) return rc;
   if ((rc = dalloc(b, &db.out_mu, B * db.Mpad))) return rc;
   if ((rc = dalloc(b, &db.out_var, B * db.Mpad))) return rc;
-  if (hipHostMalloc((void**)&b->h_mu, B * db.Mpad * sizeof(double)) != hipSuccess) return GPRX_OUT_OF_MEMORY;
-  if (hipHostMalloc((void**)&b->h_var, B * db.Mpad * sizeof(double)) != hipSuccess) return GPRX_OUT_OF_MEMORY;
+  if (hipHostMalloc((void**)&b->h_mu, B * db.Mpad * sizeof(double)) != hipSuccess ||
+      hipHostMalloc((void**)&b->h_var, B * db.Mpad * sizeof(double)) != hipSuccess) {
+    (void)hipGetLastError();
+    return GPRX_OUT_OF_MEMORY;
+  }
   (void)hipMemset(db.Xs, 0, B * db.Mpad * db.d * sizeof(double));
   return GPRX_OK;
 }
@@ -448,16 +454,16 @@ int gprx_ctx_create(int device, gprx_ctx** out) {
   if (const char* sd = getenv("GPRX_SIDE")) c->side = atoi(sd) != 0;
   c->sstreams.resize(c->nstreams);
   c->sevents.resize(3 * c->nstreams);
-  for (auto& st : c->sstreams)
-    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return GPRX_DEVICE_ERROR;
-  for (auto& e : c->sevents)
-    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return GPRX_DEVICE_ERROR;
-  for (auto& e : c->smarks)
-    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return GPRX_DEVICE_ERROR;
-  for (auto& st : c->gstreams)
-    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return GPRX_DEVICE_ERROR;
-  for (auto& e : c->gevents)
-    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return GPRX_DEVICE_ERROR;
+  bool ok = true;  // on failure the partly built context is torn down (null handles are skipped)
+  for (auto& st : c->sstreams) ok = ok && hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess;
+  for (auto& e : c->sevents) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+  for (auto& e : c->smarks) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+  for (auto& st : c->gstreams) ok = ok && hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess;
+  for (auto& e : c->gevents) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+  if (!ok) {
+    gprx_ctx_destroy(c);
+    return GPRX_DEVICE_ERROR;
+  }
   *out = c;
   return GPRX_OK;
 }
@@ -472,17 +478,22 @@ void gprx_ctx_destroy(gprx_ctx* c) {
     (void)hipEventDestroy(p.b);
   }
   for (auto e : c->evpool) (void)hipEventDestroy(e);
-  for (auto st : c->gstreams) {
-    (void)hipStreamSynchronize(st);
-    (void)hipStreamDestroy(st);
-  }
-  for (auto e : c->gevents) (void)hipEventDestroy(e);
-  for (auto e : c->smarks) (void)hipEventDestroy(e);
-  for (auto st : c->sstreams) {
-    (void)hipStreamSynchronize(st);
-    (void)hipStreamDestroy(st);
-  }
-  for (auto e : c->sevents) (void)hipEventDestroy(e);
+  for (auto st : c->gstreams)
+    if (st) {
+      (void)hipStreamSynchronize(st);
+      (void)hipStreamDestroy(st);
+    }
+  for (auto e : c->gevents)
+    if (e) (void)hipEventDestroy(e);
+  for (auto e : c->smarks)
+    if (e) (void)hipEventDestroy(e);
+  for (auto st : c->sstreams)
+    if (st) {
+      (void)hipStreamSynchronize(st);
+      (void)hipStreamDestroy(st);
+    }
+  for (auto e : c->sevents)
+    if (e) (void)hipEventDestroy(e);
   if (c->rbuf) (void)hipFree(c->rbuf);
   (void)hipStreamDestroy(c->stream);
   delete c;
@@ -526,6 +537,8 @@ int gprx_ctx_reset_stats(gprx_ctx* c) {
   return GPRX_OK;
 }
 
+static void batch_free(gprx_batch* b);
+
 int gprx_batch_create(gprx_ctx* c, int B, int d, int N, int M_max, gprx_batch** out) {
   if (!c || !out) return GPRX_INVALID_ARGUMENT;
   *out = nullptr;
@@ -551,8 +564,9 @@ int gprx_batch_create(gprx_ctx* c, int B, int d, int N, int M_max, gprx_batch** 
   db.nlj = gprx::lauum_jobs(db.nt);
   const size_t Bs = B;
   int rc = GPRX_OK;
-  auto fail = [&](int r) {
-    gprx_batch_destroy(b);
+  auto fail = [&](int r) {  // under c->mu: unlink here, free without re-locking
+    c->batches.erase(b);
+    batch_free(b);
     return r;
   };
   if ((rc = dalloc(b, &db.X, Bs * db.Npad * d))) return fail(rc);
@@ -582,8 +596,10 @@ int gprx_batch_create(gprx_ctx* c, int B, int d, int N, int M_max, gprx_batch** 
   if ((rc = alloc_test(b, M_max))) return fail(rc);
   if (hipHostMalloc((void**)&b->h_params, Bs * db.pst * sizeof(double)) != hipSuccess ||
       hipHostMalloc((void**)&b->h_out, Bs * (d + 3) * sizeof(double)) != hipSuccess ||
-      hipHostMalloc((void**)&b->h_status, 2 * Bs * sizeof(int)) != hipSuccess)
+      hipHostMalloc((void**)&b->h_status, 2 * Bs * sizeof(int)) != hipSuccess) {
+    (void)hipGetLastError();
     return fail(set_err(c, GPRX_OUT_OF_MEMORY, "hipHostMalloc failed"));
+  }
   // zero padding of X / Y (pad columns never enter a result; kept finite)
   if (hipMemset(db.X, 0, Bs * db.Npad * d * sizeof(double)) != hipSuccess ||
       hipMemset(db.Y, 0, Bs * db.Npad * sizeof(double)) != hipSuccess ||
@@ -595,12 +611,9 @@ int gprx_batch_create(gprx_ctx* c, int B, int d, int N, int M_max, gprx_batch** 
   return GPRX_OK;
 }
 
-void gprx_batch_destroy(gprx_batch* b) {
-  if (!b) return;
-  if (b->ctx) {
-    std::lock_guard<std::mutex> g(b->ctx->mu);
-    b->ctx->batches.erase(b);
-  }
+// Frees a batch that is no longer in its context's set (the caller holds no lock, or the creating
+// call's own lock: gprx_batch_create's failure path).
+static void batch_free(gprx_batch* b) {
   if (b->ctx) (void)hipSetDevice(b->ctx->device);
   if (b->ctx) (void)hipStreamSynchronize(b->ctx->stream);
   for (int i = 0; i < 4; ++i)
@@ -612,6 +625,15 @@ void gprx_batch_destroy(gprx_batch* b) {
   if (b->h_var) (void)hipHostFree(b->h_var);
   if (b->h_status) (void)hipHostFree(b->h_status);
   delete b;
+}
+
+void gprx_batch_destroy(gprx_batch* b) {
+  if (!b) return;
+  if (b->ctx) {
+    std::lock_guard<std::mutex> g(b->ctx->mu);
+    b->ctx->batches.erase(b);
+  }
+  batch_free(b);
 }
 
 int gprx_batch_dims(const gprx_batch* b, int* B, int* d, int* N, int* M_max) {

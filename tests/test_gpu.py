@@ -407,3 +407,16 @@ def test_cp_all_26_outputs_n512(gprx, ctx):
     for s in (0, 8, 21, 22):  # a constant coordinate, cart v_y, pole omega_x, pole v_y
         check_slot(r, s, tr["X"], Y[s], th, tr["Xs"], ctx.dist_mode)
     b.close()
+
+
+def test_out_of_memory_batch_is_an_error_not_a_hang(gprx, ctx, golden_dir):
+    """A batch larger than HBM fails with GPRX_OUT_OF_MEMORY (its partial allocations released
+    under the context's own lock) and the context stays usable."""
+    with pytest.raises(gprx.GPRXError) as e:
+        gprx.GPBatch(4000, 26, 4096, 0, ctx=ctx)  # 4000 x 4 x 134 MB of matrices
+    assert e.value.status == 4
+    z = np.load(golden_dir / "p1_n50.npz")
+    b = gprx.GPBatch(1, z["X"].shape[0], z["X"].shape[1], 0, ctx=ctx)
+    b.set_train(z["X"], z["Y"][:1])
+    assert b.run(z["theta"][None])["status"][0] == 0
+    b.close()
