@@ -420,3 +420,35 @@ def test_out_of_memory_batch_is_an_error_not_a_hang(gprx, ctx, golden_dir):
     b.set_train(z["X"], z["Y"][:1])
     assert b.run(z["theta"][None])["status"][0] == 0
     b.close()
+
+
+def test_threads_share_a_context(gprx, ctx, golden_dir):
+    """Threading contract (include/gprx.h): calls on one context from several host threads
+    serialise on its mutex (ctypes releases the GIL) and give the serial results bit for bit."""
+    import threading
+
+    names = ["p1_n50", "cp_n64", "p2_n100", "fb_n64"]
+    zs = [np.load(golden_dir / f"{n}.npz") for n in names]
+    batches = []
+    for z in zs:
+        b = gprx.GPBatch(z["Y"].shape[0], z["X"].shape[0], z["X"].shape[1], z["Xs"].shape[1], ctx=ctx)
+        b.set_train(z["X"], z["Y"])
+        b.set_test(z["Xs"])
+        batches.append(b)
+    serial = [b.run(np.tile(z["theta"], (z["Y"].shape[0], 1)), grad=True, predict=True) for b, z in zip(batches, zs)]
+    got = [None] * len(zs)
+
+    def work(i):
+        for _ in range(5):
+            got[i] = batches[i].run(np.tile(zs[i]["theta"], (zs[i]["Y"].shape[0], 1)), grad=True, predict=True)
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(len(zs))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=60)
+    for i in range(len(zs)):
+        for k in ("mll", "grad", "mu", "var"):
+            np.testing.assert_array_equal(got[i][k], serial[i][k])
+    for b in batches:
+        b.close()
