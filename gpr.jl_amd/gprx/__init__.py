@@ -4,10 +4,10 @@ from . import _lib
 from ._lib import GPRXError, NotPositiveDefinite, DIST_DIRECT, DIST_EXPANDED
 from .batch import Context, GPBatch, default_context
 from .gp import GP, GPE, SEArd, MeanZero, MeanFunction, predict_f, predict_y
-from .rollout import predictdynamicsmin, predictdynamicsmin_batch, rollout_min
+from .rollout import predictdynamics, predictdynamicsmin, predictdynamicsmin_batch, rollout_min
 
 __all__ = [
     "Context", "GPBatch", "default_context", "GP", "GPE", "SEArd", "MeanZero", "MeanFunction",
     "predict_f", "predict_y", "GPRXError", "NotPositiveDefinite", "DIST_DIRECT", "DIST_EXPANDED",
-    "predictdynamicsmin", "predictdynamicsmin_batch", "rollout_min",
+    "predictdynamics", "predictdynamicsmin", "predictdynamicsmin_batch", "rollout_min",
 ]

@@ -1,5 +1,7 @@
-"""Rollouts in minimal coordinates: predictdynamicsmin (examples/utils/predictdynamics.jl:30-102)
-for many trajectories in one device launch (gprx_rollout_min, include/gprx.h).
+"""Rollouts.  Minimal coordinates: predictdynamicsmin (examples/utils/predictdynamics.jl:30-102)
+for many trajectories in one device launch (gprx_rollout_min, include/gprx.h).  Maximal
+coordinates: predictdynamics (:7-22) with batched mean-only predictions per step and the physics
+(projectv!, updatestate!) injected by the caller.
 
 The reference calls `predict_y(gp, obs)[1][1]` once per GP per step per test trajectory
 (predictdynamics.jl:44,58,75,90) -- G x steps x testsamples single-point predictions, each with
@@ -132,3 +134,40 @@ def predictdynamicsmin_batch(mech: str, gps, startobservations, steps: int, uses
     (e.g. P2noise.jl(min):73-76) in one launch: (T, 13 nbodies) predicted CStates."""
     fin = rollout_min(mech, [list(gps)], startobservations, steps, usesin, dt)
     return np.stack([final_cstate(mech, f[0::2], lengths) for f in fin])
+
+
+def predictdynamics(gps, startobservations, steps: int, getvw, advance, prior_mean=None):
+    """predictdynamics(mechanism, gps, startobservation, steps, getvω) for T maximal-coordinate
+    trajectories at once (examples/utils/predictdynamics.jl:7-22).
+
+    Per step the G GPs predict the next-step velocities at all T current CStates in ONE mean-only
+    device evaluation (no variance: the reference discards it), instead of G x T single-point
+    predict_y calls.  The physics stays on the host and is injected:
+      gps               a GPBatch whose G slots share the training states (one trial's outputs,
+                        CPnoise.jl:37-43), or a list of GPEs
+      startobservations (T, d) CStates
+      getvw(mu)         mu (G,) -> (vcurr, wcurr)             (the experiment's getvω)
+      advance(s, v, w)  one trajectory's state (d,), predicted v, w -> (next state (d,), projection
+                        error)  -- projectv! + updatestate! in the reference (ConstrainedDynamics)
+      prior_mean        optional callable (d, T) -> (G, T) prior means added to the GP means for a
+                        GPBatch (a GPE adds its own mean)
+    Returns (final states (T, d), mean projection error per trajectory (T,))."""
+    S = np.array(startobservations, dtype=np.float64)
+    if S.ndim == 1:
+        S = S[None, :]
+    T = S.shape[0]
+    err = np.zeros(T)
+    for _ in range(steps):
+        obs = np.ascontiguousarray(S.T)  # (d, T)
+        if isinstance(gps, GPBatch):
+            gps.set_test(obs)
+            mu, _ = gps.predict(variance=False)  # (G, T)
+            if prior_mean is not None:
+                mu = mu + np.asarray(prior_mean(obs))
+        else:
+            mu = np.stack([g.predict_y_mean(obs) for g in gps])
+        for t in range(T):
+            v, w = getvw(mu[:, t])
+            S[t], e = advance(S[t], v, w)
+            err[t] += e
+    return S, err / max(steps, 1)

@@ -219,3 +219,50 @@ def test_predictdynamicsmin_gpe_mirror():
     gm = gprx.GP(tr["X"], tr["Y"][0], gprx.MeanFunction(lambda x: 0.0), gprx.SEArd(theta[1:-1], theta[-1]))
     with pytest.raises(NotImplementedError):
         R.predictdynamicsmin("P2", [gm, gps[1]], tr["start"][0], 3, usesin=True)
+
+
+@pytest.mark.gpu
+def test_predictdynamics_maximal_batched_matches_oracle():
+    """predictdynamics.jl:7-22 with the physics injected: per step one mean-only evaluation of the
+    trial's G GPs at all T CStates; an explicit-Euler 'advance' stands in for projectv! +
+    updatestate!.  Against the same loop on the oracle's predictive means."""
+    import gprx
+    import gprx.rollout as R
+
+    D = _data()
+    tr = D.make_trial("P2", 256, 8, seed=31)
+    th = D.theta0("P2", 256)
+    G = tr["Y"].shape[0]
+    b = gprx.GPBatch(G, 26, 256, 8)
+    b.set_train(tr["X"], tr["Y"])
+    assert np.all(b.run(np.tile(th, (G, 1)))["status"] == 0)
+    idx = D.VW_INDICES["P2"]  # outputs = v_y, v_z, omega_x of both bodies (1-based CState entries)
+
+    def getvw(mu):
+        return mu[[0, 1, 3, 4]], mu[[2, 5]]
+
+    def advance(s, v, w):
+        s = s.copy()
+        for k, i in enumerate([9, 10, 22, 23]):
+            s[i - 1] = v[k]
+        s[10], s[23] = w[0], w[1]
+        s[1] += 0.01 * s[8]
+        s[2] += 0.01 * s[9]
+        s[14] += 0.01 * s[21]
+        s[15] += 0.01 * s[22]
+        return s, 0.0
+
+    start = tr["Xs"].T.copy()  # (T, 26)
+    got, err = R.predictdynamics(b, start, 5, getvw, advance)
+    mode = b.ctx.dist_mode
+    alphas = [O.lml(tr["X"], tr["Y"][g], th, mode)[2]["alpha"] for g in range(G)]
+    il2, sf2, _, _ = O.kernel_params(th, 26)
+    S = start.copy()
+    for _ in range(5):
+        Ks = sf2 * np.exp(-O.weighted_r(O.dist_stack(tr["X"], S.T, mode), il2) * 0.5)  # N x T
+        mu = np.stack([Ks.T @ alphas[g] for g in range(G)])
+        for t in range(S.shape[0]):
+            S[t], _ = advance(S[t], *getvw(mu[:, t]))
+    assert idx == [9, 10, 22, 23, 11, 24]
+    np.testing.assert_allclose(got, S, rtol=1e-9, atol=1e-10)
+    assert np.all(err == 0.0)
