@@ -1574,16 +1574,25 @@ __device__ __forceinline__ void lauum_unit(const DevBatch& db, int slot, int pr,
     // G in place of acc:  Kf recomputed from r = n_r + n_c - 2 sum_p il2_p xc_pr xc_pc (MFMA, one
     // 16 x 16 block at a time; the same centred points as the distance sums below)
 #pragma unroll
-    for (int a = 0; a < QM; ++a)
+    for (int a = 0; a < QM; ++a) {
+      // cross terms of row block a against the 4 column blocks: 4 independent MFMA chains over
+      // the (unrolled, predicated) dimension steps, so the LDS operand loads of the next step
+      // overlap the current step's MFMAs
+      d4 cr4[QN];
 #pragma unroll
-      for (int b = 0; b < QN; ++b) {
-        d4 cr = (d4){0.0, 0.0, 0.0, 0.0};
-        for (int s2 = 0; s2 < KS; ++s2) {
+      for (int b = 0; b < QN; ++b) cr4[b] = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int s2 = 0; s2 < (DMAX + 3) / 4; ++s2) {
+        if (s2 < KS) {
           const int k = 4 * s2 + lk;
           const double xa = wl[k < d ? k : 0] * xr[(16 * a + lr) * xs + k];  // xr = 0 for k >= d
-          const double xb = xc[(16 * b + lr) * xs + k];
-          cr = mfma(xb, xa, cr);  // cr[q] = sum_p il2 x_{p,16a+lr} x_{p,16b+lk+4q}
+#pragma unroll
+          for (int b = 0; b < QN; ++b) cr4[b] = mfma(xc[(16 * b + lr) * xs + k], xa, cr4[b]);
         }
+      }
+#pragma unroll
+      for (int b = 0; b < QN; ++b) {
+        const d4 cr = cr4[b];  // cr[q] = sum_p il2 x_{p,16a+lr} x_{p,16b+lk+4q}
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int r = 16 * a + lr, c = 16 * b + lk + 4 * q;
@@ -1604,6 +1613,7 @@ __device__ __forceinline__ void lauum_unit(const DevBatch& db, int slot, int pr,
           acc[a][b][q] = G;
         }
       }
+    }
     // row sums R (row 16a + lr over the tile's 64 columns), column sums C (column 16b + lk + 4q
     // over the 64 rows)
     double R[QM], Cs[QN][4];
