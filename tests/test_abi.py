@@ -67,3 +67,13 @@ def test_ctx_create_fails_cleanly_without_gpu():
     h = C.c_void_p()
     rc = L.lib.gprx_ctx_create(0, C.byref(h))
     assert rc in (L.DEVICE_ERROR, L.INVALID_ARGUMENT) and not h.value
+
+
+def test_null_handles_are_invalid_arguments():
+    """Every entry point rejects null handles with GPRX_INVALID_ARGUMENT (no GPU needed)."""
+    assert L.lib.gprx_rollout_min(None, 2, 0, 0.01, 5, 1, None, None, 1, None, None, None) == L.INVALID_ARGUMENT
+    assert L.lib.gprx_batch_run(None, None, 0, None, None, None, None, None, None) == L.INVALID_ARGUMENT
+    assert L.lib.gprx_batch_predict(None, None, None) == L.INVALID_ARGUMENT
+    assert L.lib.gprx_gp_lml_grad(None, None, None, None) == L.INVALID_ARGUMENT
+    assert L.lib.gprx_gp_predict(None, None, 1, None, None) == L.INVALID_ARGUMENT
+    assert L.lib.gprx_gp_batch(None) is None
