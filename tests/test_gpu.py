@@ -452,3 +452,41 @@ def test_threads_share_a_context(gprx, ctx, golden_dir):
             np.testing.assert_array_equal(got[i][k], serial[i][k])
     for b in batches:
         b.close()
+
+
+def test_threads_with_own_contexts(gprx, golden_dir):
+    """The reference's pattern (Threads.@threads over trials, core.jl:28) with one context per
+    thread on the same device: each context's stream runs concurrently with the others and every
+    thread reproduces the serial results bit for bit."""
+    import threading
+
+    z = np.load(golden_dir / "p2_n100.npz")
+    G = z["Y"].shape[0]
+    th = np.tile(z["theta"], (G, 1))
+    ref_ctx = gprx.Context(0)
+    b0 = gprx.GPBatch(G, z["X"].shape[0], z["X"].shape[1], z["Xs"].shape[1], ctx=ref_ctx)
+    b0.set_train(z["X"], z["Y"])
+    b0.set_test(z["Xs"])
+    ref = b0.run(th, grad=True, predict=True)
+    b0.close()
+    ref_ctx.close()
+    got = [None] * 4
+
+    def work(i):
+        c = gprx.Context(0)
+        b = gprx.GPBatch(G, z["X"].shape[0], z["X"].shape[1], z["Xs"].shape[1], ctx=c)
+        b.set_train(z["X"], z["Y"])
+        b.set_test(z["Xs"])
+        for _ in range(5):
+            got[i] = b.run(th, grad=True, predict=True)
+        b.close()
+        c.close()
+
+    ts = [threading.Thread(target=work, args=(i,)) for i in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=60)
+    for i in range(4):
+        for k in ("mll", "grad", "mu", "var"):
+            np.testing.assert_array_equal(got[i][k], ref[k])
