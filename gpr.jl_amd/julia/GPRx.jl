@@ -72,7 +72,10 @@ function check(rc::Cint, gp)
     rc == OK || error("gprx device error ($rc)")
 end
 
-function GaussianProcesses.update_mll!(gp::GPE{<:Any,<:Any,<:Mean,<:SEArd}; kwargs...)
+# The varargs absorb GaussianProcesses' optional positional arguments (e.g. the precompute buffer
+# that optimize! passes to update_target_and_dtarget!) so these methods win dispatch for every
+# call form.
+function GaussianProcesses.update_mll!(gp::GPE{<:Any,<:Any,<:Mean,<:SEArd}, args...; kwargs...)
     m = Ref{Float64}(0.0)
     check(ccall((:gprx_gp_lml, LIB), Cint, (Ptr{Cvoid}, Ptr{Float64}, Ref{Float64}),
                 handle(gp).ptr, theta(gp), m), gp)
@@ -81,7 +84,7 @@ function GaussianProcesses.update_mll!(gp::GPE{<:Any,<:Any,<:Mean,<:SEArd}; kwar
     gp
 end
 
-function GaussianProcesses.update_target_and_dtarget!(gp::GPE{<:Any,<:Any,<:Mean,<:SEArd}; kwargs...)
+function GaussianProcesses.update_target_and_dtarget!(gp::GPE{<:Any,<:Any,<:Mean,<:SEArd}, args...; kwargs...)
     m = Ref{Float64}(0.0)
     g = zeros(length(theta(gp)))
     check(ccall((:gprx_gp_lml_grad, LIB), Cint, (Ptr{Cvoid}, Ptr{Float64}, Ref{Float64}, Ptr{Float64}),
