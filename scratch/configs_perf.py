@@ -5,7 +5,7 @@ sys.path.insert(0, '/root/repo/gpr.jl_amd'); sys.path.insert(0, '/root/repo')
 import numpy as np, gprx
 from gprx import data
 ctx = gprx.Context(0)
-cases = [("P1", 50, 64, 3, 256), ("CP", 512, 512, 26, 8), ("P2", 2048, 2048, 6, 32), ("FB", 4096, 512, 12, 4)]
+cases = [(m, n, k, g, t) for m, n, k, g, t in [("P1", 50, 64, 3, 256), ("CP", 512, 512, 26, 8), ("CP", 512, 512, 26, 16), ("P2", 2048, 2048, 6, 32), ("FB", 4096, 512, 12, 4), ("FB", 4096, 512, 12, 8)]]
 for mech, N, key, G, trials in cases:
     trs = [data.make_trial(mech, N, 100, seed=data.trial_seed(mech, t)) for t in range(trials)]
     Ysel = (lambda tr: tr["Xcurr"]) if G == 26 else (lambda tr: tr["Y"])
