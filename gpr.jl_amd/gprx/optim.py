@@ -8,8 +8,12 @@ the reference tree; Manifest.toml pins the versions].
 Each evaluation is one device call (gprx_gp_lml / gprx_gp_lml_grad through GPE).  The objective
 follows GaussianProcesses' get_optim_target: minimise -mll; a failed evaluation (not positive
 definite, ArgumentError, non-finite hyper-parameters) counts as +Inf and the parameters are
-restored.  Besides the reference's wall-clock cap, `max_evals` gives the deterministic
-evaluation budget SURVEY.md section 8d asks for.
+restored.  Convergence follows Optim's assess_convergence with its defaults (g_abstol = 1e-8,
+x_abstol = f_abstol = 0, i.e. an exact repeat of x or f also stops; allow_f_increases = true); a
+failed line search moves x by the search's last step and stops before the gradient evaluation.
+Besides the reference's wall-clock cap, `max_evals` gives the deterministic evaluation budget
+SURVEY.md section 8d asks for.  `gprx.batch.GPBatch.optimize` runs the same algorithm on the
+device (k_lbfgs), one lock-step round per batch evaluation.
 """
 from __future__ import annotations
 
@@ -40,19 +44,21 @@ class BackTracking:
         iterfinitemax = -math.log2(np.finfo(float).eps)
         a1 = a2 = alpha_0
         phix0, phix1 = phi_0, (yield a1)
-        it_fin = 0
+        it_fin = 1  # LineSearches: iterfinite = 1, so at most iterfinitemax - 1 halvings
         while not math.isfinite(phix1) and it_fin < iterfinitemax:
             it_fin += 1
             a1 = a2
             a2 = a1 / 2
             phix1 = yield a2
         it = 0
-        while phix1 > phix0 + self.c_1 * a2 * dphi_0:
+        # sufficient decrease and the quadratic model are both anchored at phi(0) = phi_0; phix0
+        # (the previous trial value) only enters the cubic model
+        while phix1 > phi_0 + self.c_1 * a2 * dphi_0:
             it += 1
             if it > self.iterations:
-                raise LineSearchError(a2)
+                raise LineSearchError(a2, phix1)
             if self.order == 2 or it == 1:
-                atmp = _div(-(dphi_0 * a2 * a2), 2 * (phix1 - phix0 - dphi_0 * a2))
+                atmp = _div(-(dphi_0 * a2 * a2), 2 * (phix1 - phi_0 - dphi_0 * a2))
             else:
                 div = _div(1.0, a1 * a1 * a2 * a2 * (a2 - a1))
                 a = (a1 * a1 * (phix1 - phi_0 - dphi_0 * a2) - a2 * a2 * (phix0 - phi_0 - dphi_0 * a1)) * div
@@ -80,9 +86,10 @@ def _drive(gen, fn):
 
 
 class LineSearchError(Exception):
-    def __init__(self, alpha):
+    def __init__(self, alpha, phi=math.nan):
         super().__init__("line search failed to converge")
         self.alpha = alpha
+        self.phi = phi  # phi(alpha): the last value the search evaluated
 
 
 def _div(a, b) -> float:
@@ -196,6 +203,8 @@ def lbfgs_steps(x0, method: LBFGS | None = None, options: Options | None = None)
         fx, g = yield ("fg", x)
         pseudo = 0
         converged = bool(np.max(np.abs(g)) <= options.g_abstol)
+        if converged:
+            stopped = "g_tol"
         while not converged and it < options.iterations:
             it += 1
             pseudo += 1
@@ -215,9 +224,16 @@ def lbfgs_steps(x0, method: LBFGS | None = None, options: Options | None = None)
             except StopIteration as e:
                 alpha, ls_ok = e.value[0], True
             except LineSearchError as e:
-                alpha, ls_ok = e.alpha, False
+                alpha, ls_ok, ls_phi = e.alpha, False, e.phi
             dx = alpha * s
+            x_prev, f_prev = x, fx
             x = x + dx
+            if not ls_ok:
+                # Optim's update_state! reports the failed search and the loop breaks before
+                # update_g!: x has moved, the objective's value cache holds phi(alpha)
+                fx = float(ls_phi)
+                stopped = "linesearch"
+                break
             budget("g")
             fx, g = yield ("fg", x)
             dg = g - g_prev
@@ -228,10 +244,15 @@ def lbfgs_steps(x0, method: LBFGS | None = None, options: Options | None = None)
                 dxh[i] = dx.copy()
                 dgh[i] = dg.copy()
                 rho[i] = r
-            if np.max(np.abs(g)) <= options.g_abstol:
-                converged, stopped = True, "g_tol"
-            elif not ls_ok:
-                stopped = "linesearch"
+            # assess_convergence with Optim's defaults x_tol = f_tol = 0 (exact repeats) and g_tol
+            with np.errstate(invalid="ignore"):
+                if np.max(np.abs(g)) <= options.g_abstol:
+                    converged, stopped = True, "g_tol"
+                elif np.max(np.abs(x - x_prev)) <= 0.0:
+                    converged, stopped = True, "x_tol"
+                elif abs(fx - f_prev) <= 0.0:
+                    converged, stopped = True, "f_tol"
+            if converged:
                 break
             if not math.isnan(options.time_limit) and time.time() - t0 > options.time_limit:
                 stopped = "time_limit"

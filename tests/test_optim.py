@@ -38,6 +38,22 @@ def test_backtracking_quadratic_interpolation_step():
     assert a == pytest.approx(0.3) and v == pytest.approx(0.0, abs=1e-15)
 
 
+def test_backtracking_anchors_every_step_at_phi0():
+    # LineSearches 7.1.1: the sufficient-decrease test and the quadratic model use phi(0), not the
+    # previous trial value.  phi(1) = 10 -> a = 0.1 (clamped); phi(0.1) = 0.15 -> the quadratic
+    # through (0, 0), slope -1, (0.1, 0.15) has its minimum at 0.02 (anchoring at phi(1) would give
+    # a negative step, clamped to 0.01)
+    vals = {1.0: 10.0, 0.1: 0.15}
+    seen = []
+
+    def phi(a):
+        seen.append(a)
+        return vals.get(a, -0.1)
+
+    a, v = BackTracking()(phi, 1.0, 0.0, -1.0)
+    assert seen[:2] == [1.0, 0.1] and a == pytest.approx(0.02, rel=1e-12) and v == -0.1
+
+
 def test_backtracking_recovers_from_infinite_values():
     phi = lambda a: math.inf if a > 0.2 else (a - 0.1) ** 2
     a, v = BackTracking()(phi, 1.0, 0.01, -0.2)
