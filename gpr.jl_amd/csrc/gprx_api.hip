@@ -1,6 +1,7 @@
 // gprx_api.hip -- C ABI (include/gprx.h) over the gfx950 kernels: context/stream ownership,
 // batch workspaces in HBM, the per-evaluation launch sequence, status mapping, profiling.
 #include <cfloat>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -146,6 +147,7 @@ DevBatch sub_batch(const DevBatch& db, int s0, int cnt) {
   v.zp += s * 2 * db.nt * (size_t)db.Npad;
   v.alpha += s * db.Npad;
   v.params += s * db.pst;
+  v.theta += s * (db.d + 2);
   v.logdet_part += s * db.nt;
   v.grad_part += s * db.ngu * db.gps;
   v.Xs += s * db.Mpad * db.d;
@@ -581,6 +583,7 @@ int gprx_batch_create(gprx_ctx* c, int B, int d, int N, int M_max, gprx_batch** 
   if ((rc = dalloc(b, &db.zp, Bs * 2 * db.nt * (size_t)db.Npad))) return fail(rc);
   if ((rc = dalloc(b, &db.alpha, Bs * db.Npad))) return fail(rc);
   if ((rc = dalloc(b, &db.params, Bs * db.pst))) return fail(rc);
+  if ((rc = dalloc(b, &db.theta, Bs * (d + 2)))) return fail(rc);
   if ((rc = dalloc(b, &db.logdet_part, Bs * db.nt))) return fail(rc);
   if ((rc = dalloc(b, &db.grad_part, Bs * db.ngu * db.gps))) return fail(rc);
   if ((rc = dalloc(b, &db.out, Bs * (d + 3)))) return fail(rc);
@@ -727,24 +730,13 @@ int gprx_batch_run(gprx_batch* b, const double* theta, unsigned flags, double* m
     db.diag_variant = dv ? atoi(dv) : 2;  // blocked MFMA diagonal kernel (measured fastest)
   }
   const int d = db.d, B = db.B, np = d + 2;
-  // hyper-parameters -> kernel parameters, exactly as SEArd / GPE derive them:
-  //   il2 = exp(-2 log ell), sf2 = exp(2 log sf), noise = exp(2 logNoise) + eps()
-  for (int s = 0; s < B; ++s) {
-    const double* th = theta + (size_t)s * np;
-    double* P = b->h_params + (size_t)s * db.pst;
-    bool finite = true;
-    for (int q = 0; q < np; ++q) finite = finite && std::isfinite(th[q]);
-    b->h_status[s] = finite ? 0 : GPRX_INVALID_ARGUMENT;
-    b->h_status[B + s] = 0;
-    for (int p = 0; p < d; ++p) P[p] = finite ? std::exp(-2.0 * th[1 + p]) : 1.0;
-    P[d] = finite ? std::exp(2.0 * th[d + 1]) : 1.0;
-    const double sn2 = finite ? std::exp(2.0 * th[0]) : 1.0;
-    P[d + 1] = sn2 + DBL_EPSILON;
-    P[d + 2] = sn2;
-    P[d + 3] = 0.0;
-  }
-  HIPCHK(c, hipMemcpyAsync(db.params, b->h_params, (size_t)B * db.pst * sizeof(double), hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, hipMemcpyAsync(db.status, b->h_status, 2 * (size_t)B * sizeof(int), hipMemcpyHostToDevice, c->stream));
+  // hyper-parameters -> kernel parameters on the device (derive_params: SEArd / GPE's
+  // il2 = exp(-2 log ell), sf2 = exp(2 log sf), noise = exp(2 logNoise) + eps()); h_params is the
+  // pinned staging buffer (pst >= d + 2 doubles per slot)
+  memcpy(b->h_params, theta, (size_t)B * np * sizeof(double));
+  HIPCHK(c, hipMemcpyAsync(db.theta, b->h_params, (size_t)B * np * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  gprx::launch_params(db, c->stream);
+  HIPCHK(c, hipGetLastError());
   const bool want_grad = (flags & GPRX_WANT_GRAD) != 0;
   const bool want_pred = (flags & GPRX_WANT_PREDICT) != 0 && b->have_test && db.M > 0;
   {
@@ -784,6 +776,146 @@ int gprx_batch_predict(gprx_batch* b, double* mu, double* var) {
   std::lock_guard<std::mutex> g(b->ctx->mu);
   if (hipSetDevice(b->ctx->device) != hipSuccess) return GPRX_DEVICE_ERROR;
   return batch_predict_locked(b, mu, var);
+}
+
+// ---- device hyper-parameter optimisation (gprx_lbfgs.hip) ---------------------------------------
+static_assert(GPRX_STOP_ITERATIONS == gprx::LB_STOP_ITERATIONS && GPRX_STOP_G_TOL == gprx::LB_STOP_G_TOL &&
+                  GPRX_STOP_X_TOL == gprx::LB_STOP_X_TOL && GPRX_STOP_F_TOL == gprx::LB_STOP_F_TOL &&
+                  GPRX_STOP_LINESEARCH == gprx::LB_STOP_LINESEARCH && GPRX_STOP_MAX_EVALS == gprx::LB_STOP_MAX_EVALS &&
+                  GPRX_STOP_TIME_LIMIT == gprx::LB_STOP_TIME_LIMIT &&
+                  GPRX_STOP_NAN_GRADIENT == gprx::LB_STOP_NAN_GRADIENT,
+              "stop codes");
+
+void gprx_opt_defaults(gprx_opt_options* o) {
+  if (!o) return;
+  o->m = 10;
+  o->iterations = 1000;
+  o->max_evals = -1;
+  o->ls_iterations = 1000;
+  o->scaleinvH0 = 1;
+  o->refit = 1;
+  o->successive_f_tol = 1;
+  o->g_abstol = 1e-8;
+  o->time_limit = NAN;  // Optim: no limit
+  o->alphaguess = 1.0;
+  o->c_1 = 1e-4;
+  o->rho_hi = 0.5;
+  o->rho_lo = 0.1;
+}
+
+int gprx_batch_optimize(gprx_batch* b, const double* theta0, const gprx_opt_options* opt, double* theta_out,
+                        double* minimum, int* iterations, int* f_calls, int* g_calls, int* stopped, int* rounds) {
+  if (!b || !theta0) return GPRX_INVALID_ARGUMENT;
+  gprx_ctx* c = b->ctx;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!b->have_train) return set_err(c, GPRX_INVALID_ARGUMENT, "gprx_batch_optimize before gprx_batch_set_train");
+  gprx_opt_options o;
+  gprx_opt_defaults(&o);
+  if (opt) o = *opt;
+  if (o.m < 1 || o.m > 64 || o.iterations < 0 || o.ls_iterations < 0 || o.successive_f_tol < 0 || !(o.c_1 > 0.0) || !(o.rho_lo > 0.0) ||
+      !(o.rho_hi > 0.0) || !std::isfinite(o.alphaguess) || std::isnan(o.g_abstol))
+    return set_err(c, GPRX_INVALID_ARGUMENT, "gprx_batch_optimize: bad options");
+  if (hipSetDevice(c->device) != hipSuccess) return GPRX_DEVICE_ERROR;
+  DevBatch& db = b->db;
+  db.dist_mode = c->dist_mode;
+  db.want_var = 0;
+  db.ablate = 0;
+  {
+    const char* sn = getenv("GPRX_SMALL_N");
+    db.small_n = sn ? atoi(sn) : (db.B >= 32 ? 8 : 64);
+    const char* dv = getenv("GPRX_DIAGV");
+    db.diag_variant = dv ? atoi(dv) : 2;
+  }
+  const int B = db.B, n = db.d + 2;
+  gprx::LbArgs a{};
+  a.n = n;
+  a.m = o.m;
+  a.max_evals = o.max_evals;
+  a.iterations = o.iterations;
+  a.ls_iterations = o.ls_iterations;
+  a.scaleinvH0 = o.scaleinvH0 ? 1 : 0;
+  a.successive_f_tol = o.successive_f_tol;
+  a.g_abstol = o.g_abstol;
+  a.alphaguess = o.alphaguess;
+  a.c_1 = o.c_1;
+  a.rho_hi = o.rho_hi;
+  a.rho_lo = o.rho_lo;
+  // one device block: state, start points, flags, results; one pinned host mirror of the flags
+  // and results
+  const size_t wsd = (size_t)B * gprx::lb_ws_doubles(n, o.m), rd = (size_t)B * (n + 1);
+  const size_t nd = wsd + (size_t)B * n + rd, ni = (size_t)B * (gprx::LB_NI + 1 + 4);
+  char* dbuf = nullptr;
+  char* hbuf = nullptr;
+  if (hipMalloc((void**)&dbuf, nd * sizeof(double) + ni * sizeof(int)) != hipSuccess) {
+    (void)hipGetLastError();
+    return set_err(c, GPRX_OUT_OF_MEMORY, "gprx_batch_optimize: workspace");
+  }
+  if (hipHostMalloc((void**)&hbuf, rd * sizeof(double) + (size_t)B * 5 * sizeof(int)) != hipSuccess) {
+    (void)hipGetLastError();
+    (void)hipFree(dbuf);
+    return set_err(c, GPRX_OUT_OF_MEMORY, "gprx_batch_optimize: host buffer");
+  }
+  struct Free {
+    char *d, *h;
+    ~Free() {
+      (void)hipFree(d);
+      (void)hipHostFree(h);
+    }
+  } fr{dbuf, hbuf};
+  a.ws = (double*)dbuf;
+  double* th0d = a.ws + wsd;
+  a.theta0 = th0d;
+  a.result = th0d + (size_t)B * n;
+  a.iws = (int*)(a.result + rd);
+  a.active = a.iws + (size_t)B * gprx::LB_NI;
+  a.result_i = a.active + B;
+  double* h_res = (double*)hbuf;
+  int* h_act = (int*)(h_res + rd);
+  int* h_ri = h_act + B;
+  HIPCHK(c, hipMemcpyAsync(th0d, theta0, (size_t)B * n * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  gprx::launch_lbfgs(a, db, 1, c->stream);
+  const bool graph = c->use_graphs && !c->prof && n_groups(c, B) == 1;
+  const auto t0 = std::chrono::steady_clock::now();
+  int nr = 0;
+  for (;;) {
+    HIPCHK(c, hipMemcpyAsync(h_act, a.active, (size_t)B * sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    int act = 0;
+    for (int s = 0; s < B; ++s) act += h_act[s] != 0;
+    if (!act) break;
+    const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    a.time_up = (o.time_limit >= 0.0 && el > o.time_limit) ? 1 : 0;  // false for NaN
+    int rc = graph ? run_graph(b, true, false) : run_groups(b, true, false, true);
+    if (rc) return rc;
+    collect(c);
+    gprx::launch_lbfgs(a, db, 0, c->stream);
+    HIPCHK(c, hipGetLastError());
+    ++nr;
+  }
+  HIPCHK(c, hipMemcpyAsync(h_res, a.result, rd * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(h_ri, a.result_i, (size_t)B * 4 * sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  if (o.refit) {  // optimize!: set_params!(gp, minimizer); update_target!(gp)
+    gprx::launch_lbfgs_final(a, db, c->stream);
+    int rc = graph ? run_graph(b, true, false) : run_groups(b, true, false, true);
+    if (rc) return rc;
+    HIPCHK(c, hipMemcpyAsync(b->h_out, db.out, (size_t)B * (db.d + 3) * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(b->h_status, db.status, 2 * (size_t)B * sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  collect(c);
+  for (int s = 0; s < B; ++s) {
+    const double* r = h_res + (size_t)s * (n + 1);
+    if (theta_out) memcpy(theta_out + (size_t)s * n, r, n * sizeof(double));
+    if (minimum) minimum[s] = r[n];
+    const int* ri = h_ri + (size_t)s * 4;
+    if (iterations) iterations[s] = ri[0];
+    if (f_calls) f_calls[s] = ri[1];
+    if (g_calls) g_calls[s] = ri[2];
+    if (stopped) stopped[s] = ri[3];
+  }
+  if (rounds) *rounds = nr;
+  b->factored = o.refit != 0;
+  return GPRX_OK;
 }
 
 // ---- single GP ---------------------------------------------------------------------------------

@@ -2,6 +2,7 @@
 // (gprx_api.hip).  Not part of the public ABI.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <cfloat>
 #include <stddef.h>
 #include <stdint.h>
 
@@ -50,6 +51,8 @@ struct DevBatch {
   double* alpha;               // B x Npad        alpha = K^{-1} y
   double* params;              // B x pst: [0,d) il2 = exp(-2 log ell), d: sf2, d+1: noise diag
                                //          (sn2 + eps), d+2: sn2
+  double* theta;               // B x (d+2) hyper-parameters [log sn, log ell_1..d, log sf] of the
+                               //          evaluation; params derive from it on the device
   double* logdet_part;         // B x nt          sum_r log L_rr per diagonal tile
   double* grad_part;           // B x ngu x gps   per lauum unit: S_p (d), S_f, trace(W)
   double* Xs;                  // B x [Mpad][d]   test points
@@ -111,7 +114,50 @@ struct RolloutArgs {
 };
 constexpr int ROLLOUT_DMAX = 6;
 
+// hyper-parameters -> kernel parameters for one slot, exactly as SEArd / GPE derive them:
+//   il2 = exp(-2 log ell), sf2 = exp(2 log sf), noise = exp(2 logNoise) + eps();
+// a non-finite theta is an ArgumentError (status GPRX_INVALID_ARGUMENT = 2, parameters 1).
+// The one derivation every evaluation uses (k_params for gprx_batch_run, k_lbfgs for the device
+// optimiser), so both see the same device exp().
+__device__ inline void derive_params(const DevBatch& b, int slot) {
+  const int d = b.d, np = d + 2;
+  const double* th = b.theta + (size_t)slot * np;
+  double* P = b.params + (size_t)slot * b.pst;
+  bool finite = true;
+  for (int q = 0; q < np; ++q) finite = finite && isfinite(th[q]);
+  for (int p = 0; p < d; ++p) P[p] = finite ? exp(-2.0 * th[1 + p]) : 1.0;
+  P[d] = finite ? exp(2.0 * th[d + 1]) : 1.0;
+  const double sn2 = finite ? exp(2.0 * th[0]) : 1.0;
+  P[d + 1] = sn2 + DBL_EPSILON;
+  P[d + 2] = sn2;
+  P[d + 3] = 0.0;
+  b.status[slot] = finite ? 0 : 2;
+  b.info[slot] = 0;
+}
+
+// Device LBFGS (gprx_lbfgs.hip): one optimiser state machine per slot, advanced between two
+// evaluations of the batch.  n = d + 2 parameters in GaussianProcesses order, m history pairs.
+constexpr int LB_NI = 16;  // ints of state per slot
+constexpr int LB_NS = 16;  // scalar doubles of state per slot
+__host__ __device__ inline size_t lb_ws_doubles(int n, int m) { return (size_t)(10 + 2 * m) * n + 2 * m + LB_NS; }
+// stop reasons (GPRX_STOP_* in gprx.h); result_i[3] = reason | 0x100 when converged
+enum LbStop : int {
+  LB_STOP_ITERATIONS = 0, LB_STOP_G_TOL = 1, LB_STOP_X_TOL = 2, LB_STOP_F_TOL = 3, LB_STOP_LINESEARCH = 4,
+  LB_STOP_MAX_EVALS = 5, LB_STOP_TIME_LIMIT = 6, LB_STOP_NAN_GRADIENT = 7
+};
+struct LbArgs {
+  double* ws;            // B x lb_ws_doubles(n, m)
+  int* iws;              // B x LB_NI
+  const double* theta0;  // B x n
+  int* active;           // B: slot requested an evaluation / is not finished
+  double* result;        // B x (n + 1): x, f(x) = -mll
+  int* result_i;         // B x 4: iterations, f calls, g calls, stop | converged
+  int n, m, max_evals, iterations, ls_iterations, scaleinvH0, successive_f_tol, time_up;
+  double g_abstol, alphaguess, c_1, rho_hi, rho_lo;
+};
+
 // kernel launchers (gprx_kernels.hip); every launcher is asynchronous on `s`
+void launch_params(const DevBatch& b, hipStream_t s);
 void launch_gram(const DevBatch& b, hipStream_t s);
 void launch_center(const DevBatch& b, hipStream_t s);
 void launch_diag(const DevBatch& b, int jt, hipStream_t s);
@@ -128,5 +174,7 @@ void launch_pred_cross(const DevBatch& b, hipStream_t s);
 void launch_pred_mu(const DevBatch& b, hipStream_t s);
 void launch_pred_final(const DevBatch& b, hipStream_t s);
 void launch_rollout(const RolloutArgs& a, int dist_mode, hipStream_t s);
+void launch_lbfgs(const LbArgs& a, const DevBatch& db, int init, hipStream_t s);  // gprx_lbfgs.hip
+void launch_lbfgs_final(const LbArgs& a, const DevBatch& db, hipStream_t s);
 
 }  // namespace gprx

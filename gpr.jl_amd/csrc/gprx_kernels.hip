@@ -2025,6 +2025,11 @@ void launch_gram(const DevBatch& b, hipStream_t s) {
   if (b.dist_mode == 0) hipLaunchKernelGGL(k_gram<0>, dim3(grid_blocks(b.B, b.ntl)), dim3(NTHR), gram_lds(b.d), s, b);
   else hipLaunchKernelGGL(k_gram<1>, dim3(grid_blocks(b.B, b.ntl)), dim3(NTHR), gram_lds(b.d), s, b);
 }
+__global__ __launch_bounds__(64) void k_params(DevBatch b) {
+  const int slot = blockIdx.x * 64 + threadIdx.x;
+  if (slot < b.B) derive_params(b, slot);
+}
+void launch_params(const DevBatch& b, hipStream_t s) { hipLaunchKernelGGL(k_params, dim3((b.B + 63) / 64), dim3(64), 0, s, b); }
 void launch_center(const DevBatch& b, hipStream_t s) { hipLaunchKernelGGL(k_center, dim3(b.B), dim3(NTHR), 0, s, b); }
 void launch_diag(const DevBatch& b, int jt, hipStream_t s) {
   if (b.diag_variant == 1) hipLaunchKernelGGL(k_diag_w, dim3(b.B), dim3(64), 0, s, b, jt);

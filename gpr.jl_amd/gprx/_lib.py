@@ -28,6 +28,19 @@ DIST_DIRECT = 1
 MEM_HOST = 0
 MEM_DEVICE = 1
 
+STOP_NAMES = {0: "iterations", 1: "g_tol", 2: "x_tol", 3: "f_tol", 4: "linesearch", 5: "max_evals", 6: "time_limit",
+              7: "nan_gradient"}
+STOP_CONVERGED = 0x100
+
+
+class OptOptions(C.Structure):
+    """gprx_opt_options (include/gprx.h); gprx_opt_defaults fills Optim's defaults."""
+    _fields_ = [("m", C.c_int), ("iterations", C.c_int), ("max_evals", C.c_int), ("ls_iterations", C.c_int),
+                ("scaleinvH0", C.c_int), ("refit", C.c_int),
+                ("successive_f_tol", C.c_int), ("g_abstol", C.c_double), ("time_limit", C.c_double),
+                ("alphaguess", C.c_double), ("c_1", C.c_double), ("rho_hi", C.c_double), ("rho_lo", C.c_double)]
+
+
 _dp = C.POINTER(C.c_double)
 _ip = C.POINTER(C.c_int)
 _vp = C.c_void_p
@@ -51,6 +64,8 @@ SIGNATURES = {
     "gprx_batch_run": (C.c_int, [_vp, _dp, C.c_uint, _dp, _dp, _dp, _dp, _ip, _ip]),
     "gprx_batch_predict": (C.c_int, [_vp, _dp, _dp]),
     "gprx_batch_dims": (C.c_int, [_vp, _ip, _ip, _ip, _ip]),
+    "gprx_opt_defaults": (None, [C.POINTER(OptOptions)]),
+    "gprx_batch_optimize": (C.c_int, [_vp, _dp, C.POINTER(OptOptions), _dp, _dp, _ip, _ip, _ip, _ip, _ip]),
     "gprx_gp_create": (C.c_int, [_vp, _dp, C.c_int, C.c_int, _dp, C.POINTER(_vp)]),
     "gprx_gp_destroy": (None, [_vp]),
     "gprx_gp_lml": (C.c_int, [_vp, _dp, _dp]),

@@ -168,6 +168,43 @@ class GPBatch:
             L.check(rc, self.ctx.h)
         return dict(mll=mll, grad=g, mu=mu, var=var, status=st, info=info)
 
+    def optimize(self, theta0, method=None, options=None, refit: bool = True):
+        """GaussianProcesses.optimize!(gp, LBFGS(linesearch=BackTracking(order=2)), options) for
+        every slot (CPnoise.jl:41), on the device (k_lbfgs: gprx/optim.py's algorithm as a per-slot
+        state machine, lock-step over the batch).  method / options: gprx.optim.LBFGS / Options.
+        Returns (results, rounds) like gprx.optim.optimize_batch; with refit the batch ends
+        factorised at the minimisers (optimize!'s update_target!), so predict() uses them."""
+        from .optim import LBFGS, Options, Result
+
+        method = method or LBFGS()
+        options = options or Options()
+        theta0 = _f64(theta0)
+        if theta0.ndim == 1:
+            theta0 = np.broadcast_to(theta0, (self.B, self.d + 2)).copy()
+        assert theta0.shape == (self.B, self.d + 2), theta0.shape
+        ls = method.linesearch
+        if ls.order != 2:
+            raise ValueError("device optimiser: BackTracking order 2 only (the experiments' setting)")
+        o = L.OptOptions()
+        L.lib.gprx_opt_defaults(C.byref(o))
+        o.m, o.iterations, o.ls_iterations = method.m, options.iterations, ls.iterations
+        o.scaleinvH0, o.refit = int(method.scaleinvH0), int(refit)
+        o.successive_f_tol = int(options.successive_f_tol)
+        o.max_evals = -1 if options.max_evals is None else int(options.max_evals)
+        o.g_abstol, o.alphaguess = options.g_abstol, method.alphaguess
+        o.time_limit = options.time_limit  # NaN: none
+        o.c_1, o.rho_hi, o.rho_lo = ls.c_1, ls.rho_hi, ls.rho_lo
+        B, n = self.B, self.d + 2
+        th = np.empty((B, n))
+        fmin = np.empty(B)
+        its, fc, gc, stp = (np.empty(B, dtype=np.int32) for _ in range(4))
+        rounds = C.c_int(0)
+        L.check(L.lib.gprx_batch_optimize(self.h, L.dptr(theta0), C.byref(o), L.dptr(th), L.dptr(fmin), L.iptr(its),
+                                          L.iptr(fc), L.iptr(gc), L.iptr(stp), C.byref(rounds)), self.ctx.h)
+        res = [Result(th[s].copy(), float(fmin[s]), int(its[s]), int(fc[s]), int(gc[s]),
+                      bool(stp[s] & L.STOP_CONVERGED), L.STOP_NAMES[int(stp[s]) & 0xFF]) for s in range(B)]
+        return res, int(rounds.value)
+
     def predict(self, variance: bool = True):
         """Predictive mean (and variance) at the current test points from the last run's
         factorisation; variance=False returns (mu, None) without the variance GEMM."""

@@ -9,8 +9,11 @@ Each evaluation is one device call (gprx_gp_lml / gprx_gp_lml_grad through GPE).
 follows GaussianProcesses' get_optim_target: minimise -mll; a failed evaluation (not positive
 definite, ArgumentError, non-finite hyper-parameters) counts as +Inf and the parameters are
 restored.  Convergence follows Optim's assess_convergence with its defaults (g_abstol = 1e-8,
-x_abstol = f_abstol = 0, i.e. an exact repeat of x or f also stops; allow_f_increases = true); a
-failed line search moves x by the search's last step and stops before the gradient evaluation.
+x_abstol = f_abstol = 0, i.e. an exact repeat of x stops, and an exact repeat of f stops once it
+has happened on successive_f_tol + 1 = 2 successive iterations; allow_f_increases = true); a
+failed line search moves x by the search's last step and stops before the gradient evaluation;
+a non-finite gradient after an iteration ends the loop ("Terminated early due to NaN in
+gradient").
 Besides the reference's wall-clock cap, `max_evals` gives the deterministic evaluation budget
 SURVEY.md section 8d asks for.  `gprx.batch.GPBatch.optimize` runs the same algorithm on the
 device (k_lbfgs), one lock-step round per batch evaluation.
@@ -98,6 +101,16 @@ def _div(a, b) -> float:
         return float(np.float64(a) / np.float64(b))
 
 
+def _dot(a, b) -> float:
+    """Sequential sum of products, left to right without fused multiply-adds: the summation order
+    of the device optimiser's dot_ (gprx_lbfgs.hip), so host and device iterates agree bit for
+    bit.  (Julia's dot is BLAS ddot, whose blocked order is not part of the reference tree.)"""
+    s = 0.0
+    for u, v in zip(np.asarray(a, dtype=np.float64).tolist(), np.asarray(b, dtype=np.float64).tolist()):
+        s += u * v
+    return s
+
+
 def _nanmin(a, b):
     return b if math.isnan(a) else (a if math.isnan(b) else min(a, b))
 
@@ -119,6 +132,7 @@ class Options:
     iterations: int = 1000
     g_abstol: float = 1e-8
     time_limit: float = math.nan
+    successive_f_tol: int = 1
     max_evals: int | None = None  # deterministic budget (not in Optim)
 
 
@@ -146,19 +160,18 @@ def _twoloop(g, rho, dxh, dgh, m, pseudo_it, scaleinvH0):
         if index < 1:
             continue
         i = (index - 1) % m
-        alpha[i] = rho[i] * float(dxh[i] @ q)
+        alpha[i] = rho[i] * _dot(dxh[i], q)
         q -= alpha[i] * dgh[i]
     if scaleinvH0 and pseudo_it > 1:
         i = (upper - 1) % m
-        with np.errstate(divide="ignore", invalid="ignore"):  # Julia float semantics: x/0 -> Inf/NaN
-            s = (np.float64(dxh[i] @ dgh[i]) / np.float64(dgh[i] @ dgh[i])) * q
+        s = _div(_dot(dxh[i], dgh[i]), _dot(dgh[i], dgh[i])) * q  # Julia float semantics: x/0 -> Inf/NaN
     else:
         s = q.copy()
     for index in range(lower, upper + 1):
         if index < 1:
             continue
         i = (index - 1) % m
-        beta = rho[i] * float(dgh[i] @ s)
+        beta = rho[i] * _dot(dgh[i], s)
         s += dxh[i] * (alpha[i] - beta)
     return -s
 
@@ -198,6 +211,7 @@ def lbfgs_steps(x0, method: LBFGS | None = None, options: Options | None = None)
     it = 0
     fx = math.nan
     converged = False
+    counter_f_tol = 0
     try:
         budget("g")
         fx, g = yield ("fg", x)
@@ -210,11 +224,11 @@ def lbfgs_steps(x0, method: LBFGS | None = None, options: Options | None = None)
             pseudo += 1
             s = _twoloop(g, rho, dxh, dgh, m, pseudo, method.scaleinvH0)
             g_prev = g.copy()
-            dphi0 = float(g @ s)
+            dphi0 = _dot(g, s)
             if dphi0 >= 0:  # reset_search_direction!
                 pseudo = 1
                 s = -g
-                dphi0 = float(g @ s)
+                dphi0 = _dot(g, s)
             ls = method.linesearch.search(method.alphaguess, fx, dphi0)
             try:
                 a = next(ls)
@@ -237,25 +251,33 @@ def lbfgs_steps(x0, method: LBFGS | None = None, options: Options | None = None)
             budget("g")
             fx, g = yield ("fg", x)
             dg = g - g_prev
-            denom = float(dx @ dg)
+            denom = _dot(dx, dg)
             r = _div(1.0, denom)
             if not math.isinf(r):
                 i = (pseudo - 1) % m
                 dxh[i] = dx.copy()
                 dgh[i] = dg.copy()
                 rho[i] = r
-            # assess_convergence with Optim's defaults x_tol = f_tol = 0 (exact repeats) and g_tol
+            # assess_convergence with Optim's defaults x_tol = f_tol = 0 (exact repeats) and g_tol;
+            # f convergence counts only on successive iterations (Options.successive_f_tol)
             with np.errstate(invalid="ignore"):
-                if np.max(np.abs(g)) <= options.g_abstol:
-                    converged, stopped = True, "g_tol"
-                elif np.max(np.abs(x - x_prev)) <= 0.0:
-                    converged, stopped = True, "x_tol"
-                elif abs(fx - f_prev) <= 0.0:
-                    converged, stopped = True, "f_tol"
+                g_conv = bool(np.max(np.abs(g)) <= options.g_abstol)
+                x_conv = bool(np.max(np.abs(x - x_prev)) <= 0.0)
+                f_conv = bool(abs(fx - f_prev) <= 0.0)
+            counter_f_tol = counter_f_tol + 1 if f_conv else 0
+            if g_conv:
+                converged, stopped = True, "g_tol"
+            elif x_conv:
+                converged, stopped = True, "x_tol"
+            elif counter_f_tol > options.successive_f_tol:
+                converged, stopped = True, "f_tol"
             if converged:
                 break
             if not math.isnan(options.time_limit) and time.time() - t0 > options.time_limit:
                 stopped = "time_limit"
+                break
+            if not np.all(np.isfinite(g)):
+                stopped = "nan_gradient"
                 break
     except _Budget:
         stopped = "max_evals"
@@ -299,7 +321,8 @@ def optimize_batch(batch, theta0, method: LBFGS | None = None, options: Options 
     ONE device evaluation of the whole batch (value + gradient for every slot).  Each slot follows
     exactly the trajectory lbfgs_minimize would give it alone (the requests and their answers are
     the same; only the device calls are shared).  A gradient computed during the line search is
-    reused when that point is accepted.  Failed slots answer +Inf as in `optimize`.
+    reused when that point is accepted, within the same round (k_lbfgs does the same).  Failed
+    slots answer +Inf as in `optimize`.
     Returns (results, rounds)."""
     theta0 = np.asarray(theta0, dtype=np.float64)
     B, npar = theta0.shape
@@ -336,10 +359,17 @@ def optimize_batch(batch, theta0, method: LBFGS | None = None, options: Options 
         for s, req in enumerate(pending):
             if req is None:
                 continue
-            _, f, g = cache[s]
-            try:
-                pending[s] = gens[s].send(f if req[0] == "f" else (f, g.copy()))
-            except StopIteration as e:
-                pending[s] = None
-                results[s] = e.value
+            # answer from the cache, and keep answering while the slot's next request is its
+            # cached point (the accepted line-search point's gradient): one round per new point
+            while True:
+                x, f, g = cache[s]
+                try:
+                    req = gens[s].send(f if req[0] == "f" else (f, g.copy()))
+                except StopIteration as e:
+                    pending[s] = None
+                    results[s] = e.value
+                    break
+                if not np.array_equal(x, req[1]):
+                    pending[s] = req
+                    break
     return results, rounds

@@ -112,6 +112,47 @@ int gprx_batch_run(gprx_batch* batch, const double* theta, unsigned flags, doubl
 int gprx_batch_predict(gprx_batch* batch, double* mu, double* var);
 int gprx_batch_dims(const gprx_batch* batch, int* B, int* d, int* N, int* M_max);
 
+/* ---- hyper-parameter optimisation on the device ------------------------------------------- */
+/* GaussianProcesses.optimize!(gp, LBFGS(linesearch=BackTracking(order=2)), Optim.Options(...))
+ * (examples/maximal_coordinates/CPnoise.jl:41 and its 15 siblings) for every slot of a batch:
+ * Optim 1.4.1 LBFGS + LineSearches 7.1.1 BackTracking restated as a device state machine, one
+ * per slot, advanced in lock-step between evaluations of the whole batch (every evaluation
+ * carries the gradient).  Minimises -mll over theta = [log sn, log ell_1..d, log sf]; a failed
+ * evaluation (not positive definite, non-finite theta) counts as +Inf, as get_optim_target.   */
+#define GPRX_STOP_ITERATIONS 0
+#define GPRX_STOP_G_TOL 1
+#define GPRX_STOP_X_TOL 2
+#define GPRX_STOP_F_TOL 3
+#define GPRX_STOP_LINESEARCH 4
+#define GPRX_STOP_MAX_EVALS 5
+#define GPRX_STOP_TIME_LIMIT 6
+#define GPRX_STOP_NAN_GRADIENT 7 /* Optim: "Terminated early due to NaN in gradient"             */
+#define GPRX_STOP_CONVERGED 0x100 /* or-ed into stopped[] when assess_convergence succeeded */
+typedef struct gprx_opt_options {
+  int m;              /* LBFGS history length (Optim: 10)                                        */
+  int iterations;     /* Options.iterations (1000)                                               */
+  int max_evals;      /* deterministic budget of f + g evaluations per slot; < 0: none (default)  */
+  int ls_iterations;  /* BackTracking.iterations (1000)                                          */
+  int scaleinvH0;     /* LBFGS scaleinvH0 (true)                                                 */
+  int refit;          /* 1: end with one evaluation of every slot at its minimiser, as optimize!
+                         does (set_params! + update_target!); mll/predict then use it (default 1) */
+  int successive_f_tol; /* Options.successive_f_tol (1): an exact f repeat converges only after
+                           successive_f_tol + 1 successive iterations                          */
+  double g_abstol;    /* Options.g_abstol (1e-8); x_abstol = f_abstol = 0 as Optim's defaults     */
+  double time_limit;  /* seconds (the experiments use 10); NaN (default) or < 0: none.  Checked
+                         between rounds: a slot stops after the iteration that sees it expired  */
+  double alphaguess;  /* InitialStatic alpha (1.0)                                               */
+  double c_1, rho_hi, rho_lo; /* BackTracking (1e-4, 0.5, 0.1)                                   */
+} gprx_opt_options;
+void gprx_opt_defaults(gprx_opt_options* opt);
+/* theta0[B*(d+2)] start points; outputs (host, any may be NULL): theta_out[B*(d+2)] minimisers,
+ * minimum[B] = -mll at the minimiser as Optim reports it, iterations/f_calls/g_calls[B],
+ * stopped[B] = GPRX_STOP_* | GPRX_STOP_CONVERGED, rounds = batch evaluations performed
+ * (excluding the refit).  Returns GPRX_OK, or an error of the evaluations themselves
+ * (device / memory); per-slot failures are +Inf answers, not errors.                          */
+int gprx_batch_optimize(gprx_batch* batch, const double* theta0, const gprx_opt_options* opt, double* theta_out,
+                        double* minimum, int* iterations, int* f_calls, int* g_calls, int* stopped, int* rounds);
+
 /* ---- single GP: the GPE surface, a batch of one ------------------------------------------- */
 int gprx_gp_create(gprx_ctx* ctx, const double* X, int d, int N, const double* y_minus_mean,
                    gprx_gp** out);

@@ -490,3 +490,87 @@ def test_threads_with_own_contexts(gprx, golden_dir):
     for i in range(4):
         for k in ("mll", "grad", "mu", "var"):
             np.testing.assert_array_equal(got[i][k], ref[k])
+
+
+def _compare_opt(dev, host):
+    """Device LBFGS (k_lbfgs) against the host restatement (gprx.optim.optimize_batch) driven
+    through the same batch: both derive the kernel parameters on the device (derive_params) and
+    sum dot products in the same sequential order, so every decision (evaluation counts,
+    iterations, stop reason) and every iterate is bit-identical."""
+    for s, (r, h) in enumerate(zip(dev, host)):
+        assert (r.iterations, r.f_calls, r.g_calls, r.stopped_by, r.converged) == (
+            h.iterations, h.f_calls, h.g_calls, h.stopped_by, h.converged), s
+        np.testing.assert_array_equal(r.minimizer, h.minimizer)
+        assert r.minimum == h.minimum or (math.isnan(r.minimum) and math.isnan(h.minimum)), s
+
+
+@pytest.mark.parametrize("name,max_evals", [("cp_n64", 20), ("p1_n50", 40), ("p2_n100", 30)])
+def test_device_optimize_matches_host_lockstep(gprx, ctx, golden_dir, name, max_evals):
+    from gprx.optim import LBFGS, Options, optimize_batch
+
+    z = np.load(golden_dir / f"{name}.npz")
+    X, Y, th = z["X"], z["Y"], z["theta"]
+    B = Y.shape[0]
+    rng = np.random.default_rng(7)
+    th0 = np.stack([th + 0.05 * rng.standard_normal(th.shape[0]) for _ in range(B)])
+    opts = Options(max_evals=max_evals)
+    b = gprx.GPBatch(B, X.shape[0], X.shape[1], 0, ctx=ctx)
+    b.set_train(X, Y)
+    host, hr = optimize_batch(b, th0, LBFGS(), opts)
+    dev, dr = b.optimize(th0, LBFGS(), opts)
+    _compare_opt(dev, host)
+    assert dr == hr
+
+
+def test_device_optimize_to_convergence_and_refit(gprx, ctx, golden_dir):
+    """optimize! to Optim's own stop (no budget) on every slot, then update_target!: the batch is
+    left factorised at the minimisers, so predict() answers for them."""
+    from gprx.optim import LBFGS, Options, optimize_batch
+
+    z = np.load(golden_dir / "p1_n50.npz")
+    X, Y, th, Xs = z["X"], z["Y"], z["theta"], z["Xs"]
+    B = Y.shape[0]
+    b = gprx.GPBatch(B, X.shape[0], X.shape[1], Xs.shape[1], ctx=ctx)
+    b.set_train(X, Y)
+    b.set_test(Xs)
+    th0 = np.tile(th, (B, 1))
+    dev, rounds = b.optimize(th0)
+    assert rounds > 0
+    mu_dev, var_dev = b.predict()
+    host, _ = optimize_batch(b, th0, LBFGS(), Options())
+    thmin = np.stack([r.minimizer for r in dev])
+    for s in range(B):
+        assert dev[s].stopped_by in ("g_tol", "x_tol", "f_tol", "linesearch")
+        assert dev[s].minimum <= host[s].minimum + 1e-6 * max(1.0, abs(host[s].minimum))
+    r = b.run(thmin, grad=True, predict=True)
+    np.testing.assert_allclose(-r["mll"], [d.minimum for d in dev], rtol=1e-12)
+    np.testing.assert_array_equal(r["mu"], mu_dev)
+    np.testing.assert_array_equal(r["var"], var_dev)
+    for s in range(B):  # the LML at the minimiser against the oracle (the gradient there is ~0 and
+        # its ill-conditioned rounding is no parity signal)
+        f = O.fit(X, Y[s], thmin[s], None, ctx.dist_mode)
+        t = tolerances(f, O.fit(X, Y[s], thmin[s], None, 1 - ctx.dist_mode), Y[s], thmin[s])
+        assert abs(r["mll"][s] - f["mll"]) <= t["mll"]
+
+
+def test_device_optimize_failed_start_and_time_limit(gprx, ctx, golden_dir):
+    """A slot whose start is not positive definite answers +Inf with a NaN gradient: both
+    optimisers take one iteration of halvings and stop on Optim's NaN-gradient break while the
+    healthy slot runs on; a zero time limit stops every slot after its first iteration."""
+    from gprx.optim import LBFGS, Options, optimize_batch
+
+    z = np.load(golden_dir / "nonpd_p1.npz")
+    X, Y, th = z["X"], z["Y"], z["theta"]
+    good = th.copy()
+    good[0] = -2.0
+    th0 = np.stack([th, good])
+    b = gprx.GPBatch(2, X.shape[0], X.shape[1], 0, ctx=ctx)
+    b.set_train(X, Y[:2])
+    opts = Options(max_evals=80)
+    host, _ = optimize_batch(b, th0, LBFGS(), opts)
+    dev, _ = b.optimize(th0, LBFGS(), opts, refit=False)
+    _compare_opt(dev, host)
+    assert dev[0].stopped_by == "nan_gradient" and dev[0].minimum == math.inf
+    assert dev[1].stopped_by == "max_evals"
+    dev, _ = b.optimize(np.stack([good, good]), LBFGS(), Options(time_limit=0.0), refit=False)
+    assert all(r.stopped_by == "time_limit" and r.iterations == 1 for r in dev)

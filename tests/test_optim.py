@@ -150,3 +150,24 @@ def test_twoloop_and_linesearch_follow_ieee_division():
     f = lambda x: float(abs(x[0]))  # kink: identical gradients on one side
     r = lbfgs_minimize(f, lambda x: (f(x), np.array([np.sign(x[0])])), np.array([3.0]), options=Options(max_evals=20))
     assert r.f_calls + r.g_calls <= 21
+
+
+def test_f_tol_needs_successive_repeats():
+    # f is constant to the last bit while the (fake) gradient is 1e-20: BackTracking accepts the
+    # unit step (the Armijo margin c_1 * a * dphi_0 = -1e-44 vanishes next to f = 1), x moves and
+    # f repeats exactly.  Optim counts that f convergence only on successive_f_tol + 1 = 2
+    # successive iterations (optimize.jl's counter_f_tol).
+    fg = lambda x: (1.0, np.array([1e-20]))
+    args = (lambda x: 1.0, fg, np.zeros(1), LBFGS(scaleinvH0=False))
+    r = lbfgs_minimize(*args, Options(g_abstol=0.0))
+    assert r.converged and r.stopped_by == "f_tol" and r.iterations == 2
+    r0 = lbfgs_minimize(*args, Options(g_abstol=0.0, successive_f_tol=0))
+    assert r0.converged and r0.stopped_by == "f_tol" and r0.iterations == 1
+
+
+def test_nan_gradient_terminates_early():
+    # every evaluation fails (+Inf, gradient NaN as GaussianProcesses leaves it): one iteration of
+    # 51 step halvings (iterfinite 1 -> 52), the NaN step is accepted against phi(0) = Inf, and
+    # Optim's "Terminated early due to NaN in gradient" ends the loop
+    r = lbfgs_minimize(lambda x: math.inf, lambda x: (math.inf, np.full(2, np.nan)), np.zeros(2))
+    assert (r.iterations, r.f_calls, r.g_calls, r.stopped_by, r.converged) == (1, 52, 2, "nan_gradient", False)
