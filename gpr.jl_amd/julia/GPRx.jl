@@ -9,6 +9,10 @@ experiment scripts (examples/noise.jl, examples/hyperparameter.jl) stay textuall
     optimize!(gp, LBFGS(...), Options())  -> gprx_gp_lml / gprx_gp_lml_grad per evaluation
     predict_y(gp, x*)                     -> gprx_gp_predict                 (predictdynamics.jl:13)
 
+plus `GPRx.optimize_all!(gps)`: the loop `for gp in gps; optimize!(gp, LBFGS(linesearch =
+BackTracking(order=2)), Optim.Options(time_limit=10.)); end` of CPnoise.jl:37-43 as ONE
+gprx_batch_optimize call (device LBFGS, every GP of the trial in lock-step).
+
 Method names follow GaussianProcesses v0.12.4 internals (update_mll!, update_target_and_dtarget!,
 predict_f); they are [ext] — confirm against that package's source before shipping.
 Not executable in the build container (no Julia runtime).
@@ -127,6 +131,71 @@ function rollout_min(etype::String, gps::Vector{<:GPE}, startobservations::Vecto
                Cint(T), zeros(Cint, T), reduce(hcat, startobservations), fin)
     check(rc, gps)
     return [fin[:, t] for t in 1:T]
+end
+
+# gprx_opt_options (include/gprx.h): same field order and C layout
+struct OptOptions
+    m::Cint
+    iterations::Cint
+    max_evals::Cint
+    ls_iterations::Cint
+    scaleinvH0::Cint
+    refit::Cint
+    successive_f_tol::Cint
+    g_abstol::Cdouble
+    time_limit::Cdouble
+    alphaguess::Cdouble
+    c_1::Cdouble
+    rho_hi::Cdouble
+    rho_lo::Cdouble
+end
+const STOP = ("iterations", "g_tol", "x_tol", "f_tol", "linesearch", "max_evals", "time_limit", "nan_gradient")
+
+# optimize! for every GP of a trial (CPnoise.jl:37-43) in one device call: Optim LBFGS +
+# BackTracking(order=2) as k_lbfgs, one lock-step evaluation of all GPs per round.  `time_limit`
+# is per call (the reference's 10 s applies to each GP in turn).  Afterwards every GP holds its
+# minimiser (set_params! + update_mll!, as optimize! leaves it).  Returns one NamedTuple per GP.
+function optimize_all!(gps::Vector{<:GPE}; time_limit::Real=NaN, iterations::Integer=1000,
+                       max_evals::Integer=-1, g_abstol::Real=1e-8)
+    B = length(gps)
+    X1 = Matrix{Float64}(gps[1].x)
+    d, N = size(X1)
+    shared = all(gp -> gp.x == gps[1].x, gps)
+    X = shared ? X1 : reduce(hcat, [Matrix{Float64}(gp.x) for gp in gps])
+    Y = reduce(hcat, [gp.y .- GaussianProcesses.mean(gp.mean, Matrix{Float64}(gp.x)) for gp in gps])
+    th0 = reduce(hcat, [theta(gp) for gp in gps])          # (d+2) x B: slot b's theta contiguous
+    ctx = context()
+    b = Ref{Ptr{Cvoid}}(C_NULL)
+    rc = ccall((:gprx_batch_create, LIB), Cint, (Ptr{Cvoid}, Cint, Cint, Cint, Cint, Ref{Ptr{Cvoid}}),
+               ctx, B, d, N, 0, b)
+    rc == OK || error("gprx_batch_create failed ($rc)")
+    try
+        rc = ccall((:gprx_batch_set_train, LIB), Cint, (Ptr{Cvoid}, Ptr{Float64}, Int64, Ptr{Float64}, Int64, Cint),
+                   b[], X, shared ? 0 : d * N, Y, N, 0)
+        rc == OK || error("gprx_batch_set_train failed ($rc)")
+        o = Ref{OptOptions}()
+        ccall((:gprx_opt_defaults, LIB), Cvoid, (Ref{OptOptions},), o)
+        o[] = OptOptions(o[].m, iterations, max_evals, o[].ls_iterations, o[].scaleinvH0, 0, o[].successive_f_tol,
+                         g_abstol, time_limit, o[].alphaguess, o[].c_1, o[].rho_hi, o[].rho_lo)
+        thx = similar(th0)
+        fmin = zeros(B)
+        its, fc, gc, stp = (zeros(Cint, B) for _ in 1:4)
+        rounds = Ref{Cint}(0)
+        rc = ccall((:gprx_batch_optimize, LIB), Cint,
+                   (Ptr{Cvoid}, Ptr{Float64}, Ref{OptOptions}, Ptr{Float64}, Ptr{Float64}, Ptr{Cint}, Ptr{Cint},
+                    Ptr{Cint}, Ptr{Cint}, Ref{Cint}),
+                   b[], th0, o, thx, fmin, its, fc, gc, stp, rounds)
+        rc == OK || error("gprx_batch_optimize failed ($rc)")
+        for (k, gp) in enumerate(gps)   # optimize!: set_params!(gp, minimizer); update_target!(gp)
+            GaussianProcesses.set_params!(gp, thx[:, k])
+            GaussianProcesses.update_mll!(gp)
+        end
+        return [(minimizer=thx[:, k], minimum=fmin[k], iterations=Int(its[k]), f_calls=Int(fc[k]),
+                 g_calls=Int(gc[k]), converged=(stp[k] & 0x100) != 0, stopped_by=STOP[(stp[k] & 0xff) + 1])
+                for k in 1:B]
+    finally
+        ccall((:gprx_batch_destroy, LIB), Cvoid, (Ptr{Cvoid},), b[])
+    end
 end
 
 end # module
