@@ -77,3 +77,25 @@ def test_null_handles_are_invalid_arguments():
     assert L.lib.gprx_gp_lml_grad(None, None, None, None) == L.INVALID_ARGUMENT
     assert L.lib.gprx_gp_predict(None, None, 1, None, None) == L.INVALID_ARGUMENT
     assert L.lib.gprx_gp_batch(None) is None
+
+
+def test_optimizer_defaults_and_null_handle():
+    """gprx_opt_defaults fills Optim 1.4.1 / LineSearches 7.1.1 defaults (LBFGS m = 10,
+    InitialStatic alpha 1, scaleinvH0; BackTracking c_1 1e-4, rho 0.1..0.5, 1000 iterations;
+    Options g_abstol 1e-8, iterations 1000, successive_f_tol 1, no time limit); the Python
+    mirror's dataclasses agree; a null batch is an invalid argument (no GPU needed)."""
+    import ctypes as C
+    import math
+
+    from gprx.optim import LBFGS, Options
+
+    o = L.OptOptions()
+    L.lib.gprx_opt_defaults(C.byref(o))
+    m, ls, op = LBFGS(), LBFGS().linesearch, Options()
+    assert (o.m, o.iterations, o.max_evals, o.ls_iterations, o.scaleinvH0, o.refit, o.successive_f_tol) == (
+        m.m, op.iterations, -1, ls.iterations, 1, 1, op.successive_f_tol)
+    assert (o.g_abstol, o.alphaguess, o.c_1, o.rho_hi, o.rho_lo) == (op.g_abstol, m.alphaguess, ls.c_1, ls.rho_hi,
+                                                                    ls.rho_lo)
+    assert math.isnan(o.time_limit) and math.isnan(op.time_limit)
+    th = (C.c_double * 4)()
+    assert L.lib.gprx_batch_optimize(None, th, C.byref(o), None, None, None, None, None, None, None) == L.INVALID_ARGUMENT
