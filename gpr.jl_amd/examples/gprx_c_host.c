@@ -8,6 +8,8 @@
  * "key v1 v2 ..." lines with %.17g:
  *   single GP on Y row 0 (GP / update_target_and_dtarget! / predict_f):  mll, grad, mu, var
  *   the G outputs of the trial as one batch (one gprx_batch_run):        batch_mll
+ *   optimize! of every output on the device, 15-evaluation budget:       opt_min, opt_evals,
+ *                                                                        opt_theta0 (slot 0)
  * Exit status 0 on success; on failure the gprx status string goes to stderr.
  */
 #include <stdint.h>
@@ -101,6 +103,27 @@ int main(int argc, char** argv) {
   rc = gprx_batch_run(b, th, 0u, bm, NULL, NULL, NULL, NULL, NULL);
   if (rc) return fail("gprx_batch_run", rc, ctx);
   print_row("batch_mll", bm, G);
+  /* GaussianProcesses.optimize! (CPnoise.jl:41) for all G outputs in lock-step on the device */
+  gprx_opt_options opt;
+  gprx_opt_defaults(&opt);
+  opt.max_evals = 15;
+  double* thx = (double*)malloc((size_t)G * (d + 2) * sizeof(double));
+  double* fmin = (double*)malloc((size_t)G * sizeof(double));
+  int* fc = (int*)malloc((size_t)G * sizeof(int));
+  int* gc = (int*)malloc((size_t)G * sizeof(int));
+  double* ev = (double*)malloc((size_t)G * sizeof(double));
+  int rounds = 0;
+  rc = gprx_batch_optimize(b, th, &opt, thx, fmin, NULL, fc, gc, NULL, &rounds);
+  if (rc) return fail("gprx_batch_optimize", rc, ctx);
+  for (int g = 0; g < G; ++g) ev[g] = fc[g] + gc[g];
+  print_row("opt_min", fmin, G);
+  print_row("opt_evals", ev, G);
+  print_row("opt_theta0", thx, d + 2);
+  free(thx);
+  free(fmin);
+  free(fc);
+  free(gc);
+  free(ev);
   gprx_batch_destroy(b);
   gprx_ctx_destroy(ctx);
   free(X);

@@ -40,3 +40,14 @@ def test_c_host_matches_oracle(tmp_path):
     for g in range(6):
         m, _, _ = O.lml(tr["X"], tr["Y"][g], th)
         assert abs(out["batch_mll"][g] - m) <= 1e-9 * max(1.0, abs(m))
+    # the device optimiser from C equals the same call through the Python mirror, bit for bit
+    import gprx
+    from gprx.optim import LBFGS, Options
+
+    b = gprx.GPBatch(6, tr["d"], 300, 0, ctx=gprx.Context(0))
+    b.set_train(tr["X"], tr["Y"])
+    res, _ = b.optimize(np.tile(th, (6, 1)), LBFGS(), Options(max_evals=15))
+    np.testing.assert_array_equal(out["opt_min"], [r.minimum for r in res])
+    np.testing.assert_array_equal(out["opt_evals"], [r.f_calls + r.g_calls for r in res])
+    np.testing.assert_array_equal(out["opt_theta0"], res[0].minimizer)
+    assert np.all(out["opt_min"] < -out["batch_mll"])
