@@ -43,26 +43,18 @@ struct gprx_ctx {
   std::map<std::string, KStat> stats;
   std::vector<hipEvent_t> evpool;
   std::vector<PendingEv> pending;
-  int nstreams = 1;                   // slot groups run concurrently on these streams (1: measured best)
   // recursion nodes of <= this many tiles run fused in k_leaf; 0 = auto: 4 for batches of >= 32
-  // slots (fewer launches), 1 below that (the one-wave diag chain has the lowest latency)
+  // slots (fewer launches), 1 below that (GPRX_OPT_LEAF_TILES)
   int leaf_tiles = 0;
-  bool fuse_tt = true;                // TT shares the SYRK launch (env GPRX_FUSE_TT=0 to split)
-  // replay each batch's launch sequence as a hipGraph (GPRX_GRAPHS=1).  Off by default: measured
+  // recursion nodes of <= this many tiles use the 64 x 32 pair-unit GEMM; 0 = auto: 8 for batches
+  // of >= 32 slots, every node below that (GPRX_OPT_SMALL_N)
+  int small_n = 0;
+  // replay each batch's launch sequence as a hipGraph (GPRX_OPT_GRAPHS).  Off by default: measured
   // equal to direct launches at B=1..192 (the launches are queued far ahead of the GPU).
   bool use_graphs = false;
-  std::vector<hipStream_t> gstreams;  // group streams
-  std::vector<hipEvent_t> gevents;    // fork/join events (1 + nstreams)
-  int stagger = -1;                   // GPRX_STAGGER: -1 groups start together; 0 / 1 group g starts
-                                      // after group g-1's Gram / factorisation
-  std::vector<hipEvent_t> smarks;     // stagger events (nstreams)
-  std::vector<hipStream_t> sstreams;  // prediction side stream per group
-  std::vector<hipEvent_t> sevents;    // 3 per group: fork, factorised, join
   std::set<gprx_batch*> batches;      // live batches (destroyed with the context)
   void* rbuf = nullptr;               // rollout argument buffer (device), grown on demand
   size_t rcap = 0;
-  bool side = false;                  // GPRX_SIDE=1: prediction on a side stream (measured no gain:
-                                      // the big kernels fill the register file, nothing co-resides)
 };
 
 struct gprx_batch {
@@ -129,45 +121,6 @@ void timed(gprx_ctx* c, hipStream_t st, const char* name, double flops, double b
   f();
   (void)hipEventRecord(b, st);
   c->pending.push_back({name, level ? std::string(name) + "/n" + std::to_string(level) : std::string(), a, b, flops, bytes});
-}
-
-// View of slots [s0, s0+cnt) of a batch (every per-slot array is slot-major).
-DevBatch sub_batch(const DevBatch& db, int s0, int cnt) {
-  DevBatch v = db;
-  const size_t s = s0;
-  v.B = cnt;
-  v.X += s * db.Npad * db.d;
-  v.Xc += s * db.Npad * db.xs;
-  v.Y += s * db.Npad;
-  v.K += s * db.mat;
-  v.Lw += s * db.mat;
-  v.Linv += s * db.mat;
-  v.Mt += s * db.mat;
-  v.z += s * db.Npad;
-  v.zp += s * 2 * db.nt * (size_t)db.Npad;
-  v.alpha += s * db.Npad;
-  v.params += s * db.pst;
-  v.theta += s * (db.d + 2);
-  v.logdet_part += s * db.nt;
-  v.grad_part += s * db.ngu * db.gps;
-  v.Xs += s * db.Mpad * db.d;
-  v.KsT += s * db.Npad * db.Mpad;
-  v.mu_part += s * db.nt * db.Mpad;
-  v.var_part += s * db.nt * db.Mpad;
-  v.out += s * (db.d + 3);
-  v.out_mu += s * db.Mpad;
-  v.out_var += s * db.Mpad;
-  v.status += s;
-  v.info += s;
-  return v;
-}
-
-// slot groups: up to nstreams groups of >= 8 slots
-int n_groups(const gprx_ctx* c, int B) {
-  int g = B / 8;
-  if (g < 1) g = 1;
-  if (g > c->nstreams) g = c->nstreams;
-  return g;
 }
 
 void collect(gprx_ctx* c) {
@@ -280,15 +233,9 @@ void factor_rec(gprx_ctx* c, hipStream_t st, const DevBatch& db, int o, int n) {
                b_tt = Bd * 8.0 * (2.0 * m2 * m1 + m1 * m1 / 2.0), b_linv = Bd * 8.0 * (3.0 * m2 * m1 + m2 * m2 / 2.0);
   timed(c, st, "potrf_trsm", f_trsm, b_trsm, [&] { gprx::launch_gemm(db, g, st); }, n);
   gprx::GemmGeom gs{gprx::OP_SYRK, o, h, n}, gt{gprx::OP_TT, o, h, n};
-  if (c->fuse_tt) {
-    // T^T = L11^-T L21^T needs only rec(A11) and the TRSM: it runs in the SYRK's launch
-    timed(c, st, "syrk_tt", f_syrk + f_tt, b_syrk + b_tt, [&] { gprx::launch_gemm(db, gs, st, gt); }, n);
-    factor_rec(c, st, db, o + h, n - h);
-  } else {
-    timed(c, st, "potrf_syrk", f_syrk, b_syrk, [&] { gprx::launch_gemm(db, gs, st); }, n);
-    factor_rec(c, st, db, o + h, n - h);
-    timed(c, st, "trtri_tt", f_tt, b_tt, [&] { gprx::launch_gemm(db, gt, st); }, n);
-  }
+  // T^T = L11^-T L21^T needs only rec(A11) and the TRSM: it runs in the SYRK's launch
+  timed(c, st, "syrk_tt", f_syrk + f_tt, b_syrk + b_tt, [&] { gprx::launch_gemm(db, gs, st, gt); }, n);
+  factor_rec(c, st, db, o + h, n - h);
   g.op = gprx::OP_LINV21;
   timed(c, st, "trtri_linv21", f_linv, b_linv, [&] { gprx::launch_gemm(db, g, st); }, n);
 }
@@ -316,30 +263,12 @@ void predict_group(gprx_ctx* c, hipStream_t st, const DevBatch& db) {
   predict_mean_final(c, st, db);
 }
 
-// Whole evaluation of one slot group on stream `st`, with the prediction's K*^T and variance GEMM
-// on the side stream `ss` (they need only the factorisation, so they run beside alpha and the
-// gradient).  `mark` (optional) is recorded once the group's factorisation is queued (the
-// stagger point of concurrent slot groups); ev[0..2] are the fork / factorised / join events.
-void eval_group(gprx_ctx* c, hipStream_t st, const DevBatch& db, bool want_grad, bool want_pred,
-                hipEvent_t mark = nullptr, hipStream_t ss = nullptr, hipEvent_t* ev = nullptr) {
+// Whole evaluation of a batch (or a slot range of it) on stream `st`.
+void eval_group(gprx_ctx* c, hipStream_t st, const DevBatch& db, bool want_grad, bool want_pred) {
   const double Bd = db.B, nt = db.nt, Np = db.Npad, d = db.d;
-  const bool side = want_pred && ss && ev;
-  if (side) {
-    (void)hipEventRecord(ev[0], st);
-    (void)hipStreamWaitEvent(ss, ev[0], 0);
-    predict_cross(c, ss, db);
-  }
   timed(c, st, "gram", Bd * 3.0 * db.N * (double)db.N * d / 2.0, Bd * 8.0 * (Np * Np / 2.0 + Np * d),
         [&] { gprx::launch_gram(db, st); });
-  if (mark && c->stagger == 0) (void)hipEventRecord(mark, st);
   factor_rec(c, st, db, 0, db.nt);
-  if (mark && c->stagger == 1) (void)hipEventRecord(mark, st);
-  if (side) {
-    (void)hipEventRecord(ev[1], st);
-    (void)hipStreamWaitEvent(ss, ev[1], 0);
-    predict_var(c, ss, db);
-    (void)hipEventRecord(ev[2], ss);
-  }
   timed(c, st, "alpha", Bd * Np * nt, Bd * 8.0 * Np * nt, [&] { gprx::launch_alpha(db, st, 0); });
   timed(c, st, "alpha", Bd * Np * Np, Bd * 8.0 * Np * Np / 2.0, [&] { gprx::launch_alpha(db, st, 1); });
   if (want_grad)
@@ -347,15 +276,9 @@ void eval_group(gprx_ctx* c, hipStream_t st, const DevBatch& db, bool want_grad,
           Bd * 8.0 * (Np * Np / 2.0 + Np * (db.xs + 2.0)),  // minimum: Mt upper, Xc, alpha once
           [&] { gprx::launch_lauum_grad(db, st); });
   timed(c, st, "finalize", Bd * 2.0 * db.N, Bd * 16.0 * db.N, [&] { gprx::launch_finalize(db, want_grad ? 1 : 0, st); });
-  if (side) {
-    (void)hipStreamWaitEvent(st, ev[2], 0);
-    predict_mean_final(c, st, db);
-  } else if (want_pred) {
-    predict_group(c, st, db);
-  }
+  if (want_pred) predict_group(c, st, db);
 }
 
-// Fork the slot groups of `b` over the context's group streams, join back on the main stream.
 // One evaluation as a replayed hipGraph: ~40-50 dependent launches per evaluation become one
 // graph launch (captured on first use; re-captured when the batch geometry, the test set or a
 // kernel variant changes).  Used when profiling is off and the batch is one slot group.
@@ -364,14 +287,13 @@ int run_graph(gprx_batch* b, bool want_grad, bool want_pred) {
   const DevBatch& db = b->db;
   const int gi = (want_grad ? 1 : 0) + (want_pred ? 2 : 0);
   const bool same = b->gvalid[gi] && memcmp(&b->gkey[gi], &db, sizeof(DevBatch)) == 0 &&
-                    b->gkey_ctx[gi][0] == c->leaf_tiles && b->gkey_ctx[gi][1] == (int)c->fuse_tt;
+                    b->gkey_ctx[gi][0] == c->leaf_tiles && b->gkey_ctx[gi][1] == c->small_n;
   if (!same) {
     if (b->gvalid[gi]) (void)hipGraphExecDestroy(b->gexec[gi]);
     b->gvalid[gi] = false;
     hipGraph_t graph = nullptr;
     HIPCHK(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-    eval_group(c, c->stream, db, want_grad, want_pred, nullptr, c->side ? c->sstreams[0] : nullptr,
-               c->side ? &c->sevents[0] : nullptr);
+    eval_group(c, c->stream, db, want_grad, want_pred);
     const hipError_t le = hipGetLastError();
     const hipError_t ce = hipStreamEndCapture(c->stream, &graph);
     if (le != hipSuccess || ce != hipSuccess) {
@@ -383,36 +305,27 @@ int run_graph(gprx_batch* b, bool want_grad, bool want_pred) {
     HIPCHK(c, ie);
     memcpy(&b->gkey[gi], &db, sizeof(DevBatch));
     b->gkey_ctx[gi][0] = c->leaf_tiles;
-    b->gkey_ctx[gi][1] = (int)c->fuse_tt;
+    b->gkey_ctx[gi][1] = c->small_n;
     b->gvalid[gi] = true;
   }
   HIPCHK(c, hipGraphLaunch(b->gexec[gi], c->stream));
   return GPRX_OK;
 }
 
-int run_groups(gprx_batch* b, bool want_grad, bool want_pred, bool factor) {
+// One evaluation on the context stream: direct launches, or the captured graph when enabled.
+// factor = false: prediction only, from the last factorisation.
+int run_eval(gprx_batch* b, bool want_grad, bool want_pred, bool factor) {
   gprx_ctx* c = b->ctx;
-  const DevBatch& db = b->db;
-  const int G = n_groups(c, db.B);
-  HIPCHK(c, hipEventRecord(c->gevents[0], c->stream));
-  int s0 = 0;
-  for (int g = 0; g < G; ++g) {
-    const int cnt = db.B / G + (g < db.B % G ? 1 : 0);
-    hipStream_t st = c->gstreams[g];
-    HIPCHK(c, hipStreamWaitEvent(st, c->gevents[0], 0));
-    // staggered groups: group g starts when group g-1 has passed its stagger point
-    if (g > 0 && c->stagger >= 0 && factor) HIPCHK(c, hipStreamWaitEvent(st, c->smarks[g - 1], 0));
-    const DevBatch v = sub_batch(db, s0, cnt);
-    if (factor)
-      eval_group(c, st, v, want_grad, want_pred, c->stagger >= 0 ? c->smarks[g] : nullptr,
-                 c->side ? c->sstreams[g] : nullptr, c->side ? &c->sevents[3 * g] : nullptr);
-    else if (want_pred) predict_group(c, st, v);
-    HIPCHK(c, hipEventRecord(c->gevents[1 + g], st));
-    HIPCHK(c, hipStreamWaitEvent(c->stream, c->gevents[1 + g], 0));
-    s0 += cnt;
-  }
+  if (factor && c->use_graphs && !c->prof) return run_graph(b, want_grad, want_pred);
+  if (factor) eval_group(c, c->stream, b->db, want_grad, want_pred);
+  else if (want_pred) predict_group(c, c->stream, b->db);
   HIPCHK(c, hipGetLastError());
   return GPRX_OK;
+}
+
+// Per-call launch geometry from the context options and the batch size.
+void set_geometry(const gprx_ctx* c, DevBatch& db) {
+  db.small_n = c->small_n > 0 ? c->small_n : (db.B >= 32 ? 8 : 64);  // small batches: more, smaller units
 }
 
 }  // namespace
@@ -445,27 +358,6 @@ int gprx_ctx_create(int device, gprx_ctx** out) {
     delete c;
     return GPRX_DEVICE_ERROR;
   }
-  if (const char* ns = getenv("GPRX_STREAMS")) c->nstreams = atoi(ns) > 0 ? atoi(ns) : 1;
-  if (const char* ft = getenv("GPRX_FUSE_TT")) c->fuse_tt = atoi(ft) != 0;
-  if (const char* gr = getenv("GPRX_GRAPHS")) c->use_graphs = atoi(gr) != 0;
-  if (const char* lt = getenv("GPRX_LEAF")) c->leaf_tiles = atoi(lt) >= 0 && atoi(lt) <= 8 ? atoi(lt) : 0;
-  if (const char* sg = getenv("GPRX_STAGGER")) c->stagger = atoi(sg);
-  c->gstreams.resize(c->nstreams);
-  c->gevents.resize(1 + c->nstreams);
-  c->smarks.resize(c->nstreams);
-  if (const char* sd = getenv("GPRX_SIDE")) c->side = atoi(sd) != 0;
-  c->sstreams.resize(c->nstreams);
-  c->sevents.resize(3 * c->nstreams);
-  bool ok = true;  // on failure the partly built context is torn down (null handles are skipped)
-  for (auto& st : c->sstreams) ok = ok && hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess;
-  for (auto& e : c->sevents) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
-  for (auto& e : c->smarks) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
-  for (auto& st : c->gstreams) ok = ok && hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess;
-  for (auto& e : c->gevents) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
-  if (!ok) {
-    gprx_ctx_destroy(c);
-    return GPRX_DEVICE_ERROR;
-  }
   *out = c;
   return GPRX_OK;
 }
@@ -480,22 +372,6 @@ void gprx_ctx_destroy(gprx_ctx* c) {
     (void)hipEventDestroy(p.b);
   }
   for (auto e : c->evpool) (void)hipEventDestroy(e);
-  for (auto st : c->gstreams)
-    if (st) {
-      (void)hipStreamSynchronize(st);
-      (void)hipStreamDestroy(st);
-    }
-  for (auto e : c->gevents)
-    if (e) (void)hipEventDestroy(e);
-  for (auto e : c->smarks)
-    if (e) (void)hipEventDestroy(e);
-  for (auto st : c->sstreams)
-    if (st) {
-      (void)hipStreamSynchronize(st);
-      (void)hipStreamDestroy(st);
-    }
-  for (auto e : c->sevents)
-    if (e) (void)hipEventDestroy(e);
   if (c->rbuf) (void)hipFree(c->rbuf);
   (void)hipStreamDestroy(c->stream);
   delete c;
@@ -511,6 +387,25 @@ int gprx_ctx_set_dist_mode(gprx_ctx* c, int mode) {
 }
 
 int gprx_ctx_device(const gprx_ctx* c) { return c ? c->device : -1; }
+
+int gprx_ctx_set_option(gprx_ctx* c, int option, int value) {
+  if (!c) return GPRX_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> g(c->mu);
+  switch (option) {
+    case GPRX_OPT_LEAF_TILES:
+      if (value < 0 || value > 8) return set_err(c, GPRX_INVALID_ARGUMENT, "leaf tiles: 0 (auto) .. 8");
+      c->leaf_tiles = value;
+      return GPRX_OK;
+    case GPRX_OPT_SMALL_N:
+      if (value < 0) return set_err(c, GPRX_INVALID_ARGUMENT, "small_n: >= 0 (0 = auto)");
+      c->small_n = value;
+      return GPRX_OK;
+    case GPRX_OPT_GRAPHS:
+      c->use_graphs = value != 0;
+      return GPRX_OK;
+  }
+  return set_err(c, GPRX_INVALID_ARGUMENT, "unknown option");
+}
 
 int gprx_ctx_set_profiling(gprx_ctx* c, int enable) {
   if (!c) return GPRX_INVALID_ARGUMENT;
@@ -698,7 +593,7 @@ static int batch_predict_locked(gprx_batch* b, double* mu, double* var) {
   if (!b->factored) return set_err(c, GPRX_NOT_READY, "predict before a successful factorisation");
   if (!b->have_test || db.M == 0) return GPRX_OK;
   db.want_var = var != nullptr;
-  int rc = run_groups(b, false, true, false);
+  int rc = run_eval(b, false, true, false);
   if (rc) return rc;
   HIPCHK(c, hipMemcpyAsync(b->h_mu, db.out_mu, (size_t)db.B * db.Mpad * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipMemcpyAsync(b->h_var, db.out_var, (size_t)db.B * db.Mpad * sizeof(double), hipMemcpyDeviceToHost, c->stream));
@@ -721,14 +616,7 @@ int gprx_batch_run(gprx_batch* b, const double* theta, unsigned flags, double* m
   DevBatch& db = b->db;
   db.dist_mode = c->dist_mode;
   db.want_var = var != nullptr;
-  {
-    const char* ab = getenv("GPRX_ABLATE");  // timing experiments only; results are wrong when set
-    db.ablate = ab ? atoi(ab) : 0;
-    const char* sn = getenv("GPRX_SMALL_N");
-    db.small_n = sn ? atoi(sn) : (db.B >= 32 ? 8 : 64);  // small batches: more, smaller units
-    const char* dv = getenv("GPRX_DIAGV");
-    db.diag_variant = dv ? atoi(dv) : 2;  // blocked MFMA diagonal kernel (measured fastest)
-  }
+  set_geometry(c, db);
   const int d = db.d, B = db.B, np = d + 2;
   // hyper-parameters -> kernel parameters on the device (derive_params: SEArd / GPE's
   // il2 = exp(-2 log ell), sf2 = exp(2 log sf), noise = exp(2 logNoise) + eps()); h_params is the
@@ -740,8 +628,7 @@ int gprx_batch_run(gprx_batch* b, const double* theta, unsigned flags, double* m
   const bool want_grad = (flags & GPRX_WANT_GRAD) != 0;
   const bool want_pred = (flags & GPRX_WANT_PREDICT) != 0 && b->have_test && db.M > 0;
   {
-    const bool graph = c->use_graphs && !c->prof && n_groups(c, B) == 1;
-    int rc = graph ? run_graph(b, want_grad, want_pred) : run_groups(b, want_grad, want_pred, true);
+    int rc = run_eval(b, want_grad, want_pred, true);
     if (rc) return rc;
   }
   HIPCHK(c, hipMemcpyAsync(b->h_out, db.out, (size_t)B * (d + 3) * sizeof(double), hipMemcpyDeviceToHost, c->stream));
@@ -769,6 +656,19 @@ int gprx_batch_run(gprx_batch* b, const double* theta, unsigned flags, double* m
   b->factored = true;
   if (first != GPRX_OK) set_err(c, first, std::string("gprx_batch_run: ") + gprx_status_string(first));
   return first;
+}
+
+int gprx_batch_alpha(gprx_batch* b, double* alpha) {
+  if (!b || !alpha) return GPRX_INVALID_ARGUMENT;
+  gprx_ctx* c = b->ctx;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!b->factored) return set_err(c, GPRX_NOT_READY, "alpha before a successful factorisation");
+  if (hipSetDevice(c->device) != hipSuccess) return GPRX_DEVICE_ERROR;
+  const DevBatch& db = b->db;
+  HIPCHK(c, hipMemcpy2DAsync(alpha, (size_t)db.N * sizeof(double), db.alpha, (size_t)db.Npad * sizeof(double),
+                             (size_t)db.N * sizeof(double), db.B, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return GPRX_OK;
 }
 
 int gprx_batch_predict(gprx_batch* b, double* mu, double* var) {
@@ -819,13 +719,7 @@ int gprx_batch_optimize(gprx_batch* b, const double* theta0, const gprx_opt_opti
   DevBatch& db = b->db;
   db.dist_mode = c->dist_mode;
   db.want_var = 0;
-  db.ablate = 0;
-  {
-    const char* sn = getenv("GPRX_SMALL_N");
-    db.small_n = sn ? atoi(sn) : (db.B >= 32 ? 8 : 64);
-    const char* dv = getenv("GPRX_DIAGV");
-    db.diag_variant = dv ? atoi(dv) : 2;
-  }
+  set_geometry(c, db);
   const int B = db.B, n = db.d + 2;
   gprx::LbArgs a{};
   a.n = n;
@@ -872,9 +766,11 @@ int gprx_batch_optimize(gprx_batch* b, const double* theta0, const gprx_opt_opti
   double* h_res = (double*)hbuf;
   int* h_act = (int*)(h_res + rd);
   int* h_ri = h_act + B;
+  // theta, L and the factorisation flags are overwritten from here on: the batch holds no valid
+  // factorisation until the refit below has succeeded for every slot
+  b->factored = false;
   HIPCHK(c, hipMemcpyAsync(th0d, theta0, (size_t)B * n * sizeof(double), hipMemcpyHostToDevice, c->stream));
   gprx::launch_lbfgs(a, db, 1, c->stream);
-  const bool graph = c->use_graphs && !c->prof && n_groups(c, B) == 1;
   const auto t0 = std::chrono::steady_clock::now();
   int nr = 0;
   for (;;) {
@@ -885,7 +781,7 @@ int gprx_batch_optimize(gprx_batch* b, const double* theta0, const gprx_opt_opti
     if (!act) break;
     const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     a.time_up = (o.time_limit >= 0.0 && el > o.time_limit) ? 1 : 0;  // false for NaN
-    int rc = graph ? run_graph(b, true, false) : run_groups(b, true, false, true);
+    int rc = run_eval(b, true, false, true);
     if (rc) return rc;
     collect(c);
     gprx::launch_lbfgs(a, db, 0, c->stream);
@@ -896,7 +792,7 @@ int gprx_batch_optimize(gprx_batch* b, const double* theta0, const gprx_opt_opti
   HIPCHK(c, hipMemcpyAsync(h_ri, a.result_i, (size_t)B * 4 * sizeof(int), hipMemcpyDeviceToHost, c->stream));
   if (o.refit) {  // optimize!: set_params!(gp, minimizer); update_target!(gp)
     gprx::launch_lbfgs_final(a, db, c->stream);
-    int rc = graph ? run_graph(b, true, false) : run_groups(b, true, false, true);
+    int rc = run_eval(b, true, false, true);
     if (rc) return rc;
     HIPCHK(c, hipMemcpyAsync(b->h_out, db.out, (size_t)B * (db.d + 3) * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(b->h_status, db.status, 2 * (size_t)B * sizeof(int), hipMemcpyDeviceToHost, c->stream));
@@ -914,7 +810,17 @@ int gprx_batch_optimize(gprx_batch* b, const double* theta0, const gprx_opt_opti
     if (stopped) stopped[s] = ri[3];
   }
   if (rounds) *rounds = nr;
-  b->factored = o.refit != 0;
+  if (!o.refit) return GPRX_OK;
+  // the refit's per-slot status, as gprx_batch_run reports it: a minimiser that is not finite
+  // (status 2) or not positive definite (status 1) is an error of update_target!, and the batch is
+  // then not left factorised
+  int first = GPRX_OK, bad = -1;
+  for (int s = 0; s < B && first == GPRX_OK; ++s)
+    if (b->h_status[s] != GPRX_OK) first = b->h_status[s], bad = s;
+  if (first != GPRX_OK)
+    return set_err(c, first, "gprx_batch_optimize: refit at the minimiser of slot " + std::to_string(bad) + ": " +
+                                 gprx_status_string(first));
+  b->factored = true;
   return GPRX_OK;
 }
 

@@ -25,12 +25,9 @@ struct DevBatch {
   int dist_mode;               // GPRX_DIST_EXPANDED / GPRX_DIST_DIRECT
   int want_var;                // predictive variance requested (var output non-NULL); 0 skips the
                                // O(N^2 M) variance GEMM (predictdynamics.jl uses the mean only)
-  int ablate;                  // timing-only ablation bits (env GPRX_ABLATE; 0 in production)
   int small_n;                 // recursion nodes of <= small_n tiles use the 64 x 32 pair-unit GEMM
-                               // (GPRX_SMALL_N; default 8 for B >= 32, all nodes below that, where
-                               // the 64 x 64 units leave most of the chip idle); larger: 64 x 64 core
-  int diag_variant;            // 0: 4-wave k_diag, 1: one-wave k_diag_w, 2: blocked k_diag_f (default;
-                               // env GPRX_DIAGV)
+                               // (default 8 for B >= 32, all nodes below that, where the 64 x 64
+                               // units leave most of the chip idle); larger: 64 x 64 core
   int xs;                      // row stride of Xc: 16 ceil(d/16) + 1 (odd: spreads LDS banks)
   int pst;                     // stride of params per slot
   int gps;                     // stride of per-unit gradient partials (d + 2)

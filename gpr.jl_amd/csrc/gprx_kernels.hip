@@ -165,33 +165,24 @@ __device__ __forceinline__ double wave_sum(double v) {
 __device__ __forceinline__ double* zp_row(const DevBatch& db, int slot, int h) {
   return db.zp + ((size_t)slot * 2 * db.nt + h) * db.Npad;
 }
-// a diagonal tile from an LDS image: row r of X at img[r * rs + c * cs].  With a 256-thread
-// workgroup and a [256]-double scratch the 64 columns are split in 4 quarters (no serial chain);
-// call from every thread of the workgroup (contains barriers when scr != nullptr).
+// a diagonal tile from an LDS image: row r of X at img[r * rs + c * cs].  The 256-thread
+// workgroup splits the 64 columns in 4 quarters through the [256]-double scratch (no serial
+// chain); call from every thread of the workgroup (contains barriers).
 __device__ __forceinline__ void zp_diag(const DevBatch& db, int slot, int jt, const double* img, int rs, int cs,
-                                        double* scr = nullptr) {
+                                        double* scr) {
   const double* y = db.Y + (size_t)slot * db.Npad + jt * TS;
-  if (scr) {
-    const int r = threadIdx.x & 63, qc = threadIdx.x >> 6;
-    double t = 0.0;
-#pragma unroll
-    for (int c = 16 * qc; c < 16 * qc + 16; ++c) t = fma(img[r * rs + c * cs], y[c], t);  // X upper = 0
-    __syncthreads();
-    scr[qc * TS + r] = t;
-    __syncthreads();
-    if (qc == 0) {
-      zp_row(db, slot, 2 * jt)[jt * TS + r] = ((scr[r] + scr[TS + r]) + scr[2 * TS + r]) + scr[3 * TS + r];
-      zp_row(db, slot, 2 * jt + 1)[jt * TS + r] = 0.0;
-    }
-    __syncthreads();
-    return;
-  }
-  const int r = threadIdx.x;
-  if (r >= TS) return;
+  const int r = threadIdx.x & 63, qc = threadIdx.x >> 6;
   double t = 0.0;
-  for (int c = 0; c <= r; ++c) t = fma(img[r * rs + c * cs], y[c], t);
-  zp_row(db, slot, 2 * jt)[jt * TS + r] = t;
-  zp_row(db, slot, 2 * jt + 1)[jt * TS + r] = 0.0;
+#pragma unroll
+  for (int c = 16 * qc; c < 16 * qc + 16; ++c) t = fma(img[r * rs + c * cs], y[c], t);  // X upper = 0
+  __syncthreads();
+  scr[qc * TS + r] = t;
+  __syncthreads();
+  if (qc == 0) {
+    zp_row(db, slot, 2 * jt)[jt * TS + r] = ((scr[r] + scr[TS + r]) + scr[2 * TS + r]) + scr[3 * TS + r];
+    zp_row(db, slot, 2 * jt + 1)[jt * TS + r] = 0.0;
+  }
+  __syncthreads();
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -515,135 +506,23 @@ __global__ __launch_bounds__(NTHR) void k_center(DevBatch db) {
 
 // ============================================================================================
 // Leaf of the recursion: Cholesky of the 64x64 diagonal tile jt (already reduced by the SYRK
-// updates of its ancestors) and its inverse.  One workgroup per slot; lane = column c,
-// wave w owns rows 16w..16w+15 of that column in registers.  Column k is broadcast through LDS
-// (double-buffered, one barrier per step); the update uses a_rc -= a_rk * (a_ck / a_kk) on the
-// unscaled columns, scaled once at the end.  Failure (pivot <= 0 or NaN, as LAPACK dpotrf) records
-// status 1 and the 1-based global pivot index and continues with pivot 1.
-// Writes Linv[jt,jt] = L_jj^-1 and Mt[jt,jt] = L_jj^-T (full tiles, explicit zeros) and the tile's
-// sum_c log L_cc.
-// ============================================================================================
-constexpr int DS = TS + 1;
-__device__ __forceinline__ void diag_tile(const DevBatch& db, int slot, int jt) {
-  __shared__ double Ls[TS * DS];
-  __shared__ double colbuf[2][TS];
-  __shared__ double piv[TS];
-  __shared__ double rdiag[TS];
-  __shared__ double red[4];
-  __shared__ double rowbuf[2][TS];
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  const size_t ld = db.ld;
-  const double* A = db.K + (size_t)slot * db.mat + (size_t)jt * TS * ld + jt * TS;
-  for (int e = tid; e < TS * TS; e += NTHR) {
-    const int r = e & 63, c = e >> 6;
-    Ls[c * DS + r] = (r >= c) ? A[(size_t)c * ld + r] : 0.0;
-  }
-  __syncthreads();
-  double a[16];
-#pragma unroll
-  for (int q = 0; q < 16; ++q) a[q] = Ls[lane * DS + 16 * w + q];
-  int fail = -1;
-  for (int k = 0; k < TS; ++k) {
-    double* cb = colbuf[k & 1];
-    if (lane == k) {
-#pragma unroll
-      for (int q = 0; q < 16; ++q) cb[16 * w + q] = a[q];
-    }
-    __syncthreads();
-    // all reads of this step issued together, one wait
-    const double akk = cb[k];
-    const double ack = cb[lane];
-    double ark[16];
-#pragma unroll
-    for (int q = 0; q < 16; ++q) ark[q] = cb[16 * w + q];
-    const double pk = (akk > 0.0) ? akk : 1.0;
-    if (tid == 0) {
-      piv[k] = pk;
-      if (!(akk > 0.0) && fail < 0) fail = k;
-    }
-    const double t = (lane > k) ? ack * recip(pk) : 0.0;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) a[q] = fma(-ark[q], t, a[q]);
-  }
-  __syncthreads();
-  // L[r][c] = a_rc / sqrt(p_c) (r > c), sqrt(p_c) (r == c), 0 (r < c); into Ls[c][r]
-  {
-    const double sc = sqrt(piv[lane]), isc = 1.0 / sc;
-    rdiag[lane] = isc;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int r = 16 * w + q;
-      Ls[lane * DS + r] = (r > lane) ? a[q] * isc : (r == lane ? sc : 0.0);
-    }
-    if (w == 0) {
-      const double s = wave_sum(log(sc));
-      if (lane == 0) red[0] = s;
-    }
-  }
-  __syncthreads();
-  if (tid == 0) {
-    db.logdet_part[(size_t)slot * db.nt + jt] = red[0];
-    if (fail >= 0 && db.status[slot] == 0) {
-      db.status[slot] = 1;
-      db.info[slot] = jt * TS + fail + 1;
-    }
-  }
-  // X = L^-1 by forward substitution: lane = column c, wave w holds rows 16w..16w+15.
-  double x[16];
-#pragma unroll
-  for (int q = 0; q < 16; ++q) x[q] = (16 * w + q == lane) ? 1.0 : 0.0;
-  for (int kb = 0; kb < 4; ++kb) {
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int k = 16 * kb + q;
-      double* rb = rowbuf[k & 1];
-      if (w == kb) {
-        x[q] = x[q] * rdiag[k];
-        rb[lane] = x[q];
-      }
-      __syncthreads();
-      const double xr = rb[lane];
-      if (w > kb) {
-        double lk2[16];
-#pragma unroll
-        for (int q2 = 0; q2 < 16; ++q2) lk2[q2] = Ls[k * DS + 16 * w + q2];
-#pragma unroll
-        for (int q2 = 0; q2 < 16; ++q2) x[q2] = fma(-lk2[q2], xr, x[q2]);
-      } else if (w == kb) {
-#pragma unroll
-        for (int q2 = q + 1; q2 < 16; ++q2) x[q2] = fma(-Ls[k * DS + 16 * w + q2], xr, x[q2]);
-      }
-    }
-  }
-  __syncthreads();  // all reads of Ls (L) done
-#pragma unroll
-  for (int q = 0; q < 16; ++q) Ls[lane * DS + 16 * w + q] = x[q];  // Ls[c][r] = X[r][c]
-  __syncthreads();
-  double* Li = db.Linv + (size_t)slot * db.mat + (size_t)jt * TS * ld + jt * TS;
-  double* Mj = db.Mt + (size_t)slot * db.mat + (size_t)jt * TS * ld + jt * TS;
-  for (int e = tid; e < TS * TS; e += NTHR) {
-    const int r = e & 63, c = e >> 6;
-    Li[(size_t)c * ld + r] = Ls[c * DS + r];  // Linv[r][c] = X[r][c]
-    Mj[(size_t)c * ld + r] = Ls[r * DS + c];  // Mt[r][c]   = X[c][r]
-  }
-  zp_diag(db, slot, jt, Ls, 1, DS);
-}
-__global__ __launch_bounds__(NTHR) void k_diag(DevBatch db, int jt) { diag_tile(db, blockIdx.x, jt); }
-__device__ __forceinline__ void diag_tile_fast(const DevBatch& db, int slot, int jt);
-__global__ __launch_bounds__(NTHR) void k_diag_f(DevBatch db, int jt) { diag_tile_fast(db, blockIdx.x, jt); }
-// --------------------------------------------------------------------------------------------
-// Same leaf, blocked by 16 (4 waves): the 16x16 diagonal blocks are factored and inverted in
-// registers by wave 0 (lane = row / column, pivots and row values broadcast by readlane), the
-// panel TRSM / trailing SYRK and the off-diagonal blocks of the inverse run on the MFMA pipe from
-// an LDS image of the tile.  4 + 3 barrier-separated phases per panel instead of 128 steps.
+// updates of its ancestors) and its inverse, one workgroup (4 waves) per slot, blocked by 16:
+// the 16x16 diagonal blocks are factored and inverted in registers by wave 0 (lane = row /
+// column, pivots and row values broadcast by readlane), the panel TRSM / trailing SYRK and the
+// off-diagonal blocks of the inverse run on the MFMA pipe from an LDS image of the tile.
+// 4 + 3 barrier-separated phases per panel instead of 128 steps.
 //   panel P (c0 = 16P):  D = chol(A_PP), Dinv = D^-1               (wave 0)
 //                        A_iP <- A_iP Dinv^T  (i > P)              (TRSM, one wave per block)
 //                        A_ij -= A_iP A_jP^T  (i >= j > P)          (SYRK)
 //   inverse:  X_PP = Dinv_P ;  X_ij = -Dinv_i sum_{k=j}^{i-1} L_ik X_kj   by sub-diagonal i - j
-// Failure semantics as diag_tile (first pivot <= 0 or NaN; continue with pivot 1).
+// Failure (first pivot <= 0 or NaN, as LAPACK dpotrf) records status 1 and the 1-based global
+// pivot index and continues with pivot 1.  Writes Linv[jt,jt] = L_jj^-1 and Mt[jt,jt] = L_jj^-T
+// (full tiles, explicit zeros) and the tile's sum_c log L_cc.
 // 16x16x4 f64 MFMA operand maps (gfx950): A lane l = A[l&15][l>>4], B lane l = B[l>>4][l&15],
 // D lane l reg q = D[(l>>4) + 4q][l&15].
-// --------------------------------------------------------------------------------------------
+// ============================================================================================
+__device__ __forceinline__ void diag_tile_fast(const DevBatch& db, int slot, int jt);
+__global__ __launch_bounds__(NTHR) void k_diag_f(DevBatch db, int jt) { diag_tile_fast(db, blockIdx.x, jt); }
 constexpr int FS = TS + 1;  // LDS column stride of the tile images
 __device__ __forceinline__ void diag_tile_fast(const DevBatch& db, int slot, int jt) {
   __shared__ double T[TS * FS];   // T[c*FS + r] = A[r][c], then L (lower)
@@ -662,7 +541,7 @@ __device__ __forceinline__ void diag_tile_fast(const DevBatch& db, int slot, int
   double lsum = 0.0;  // wave 0: sum log l_jj
   for (int P = 0; P < 4; ++P) {
     const int c0 = 16 * P;
-    if (w == 0 && !(db.ablate & 256)) {
+    if (w == 0) {
       // ---- factor the diagonal block: lane i < 16 holds row i (a[k] = A[c0+i][c0+k]); the
       //      scaled column j is published in LDS (cb) and read back as broadcasts ----
       double* cb = cbs;  // scratch: column j of L during the factor, then the row-major L block
@@ -730,7 +609,7 @@ __device__ __forceinline__ void diag_tile_fast(const DevBatch& db, int slot, int
     // ---- TRSM: block row i > P:  A_iP <- A_iP Dinv^T   (D[r][c] = sum_k A_iP[r][k] Dinv[c][k]) ----
     {
       const int i = P + 1 + w;
-      if (i < 4 && !(db.ablate & 512)) {
+      if (i < 4) {
         d4 acc = (d4){0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
@@ -747,7 +626,7 @@ __device__ __forceinline__ void diag_tile_fast(const DevBatch& db, int slot, int
     // ---- SYRK: A_ij -= A_iP A_jP^T for P < j <= i < 4 ----
     {
       const int m = 3 - P;  // trailing blocks per edge
-      for (int t = w; t < ((db.ablate & 512) ? 0 : m * (m + 1) / 2); t += 4) {
+      for (int t = w; t < m * (m + 1) / 2; t += 4) {
         int u = t, j = 0;
         while (u >= m - j) {
           u -= m - j;
@@ -772,7 +651,7 @@ __device__ __forceinline__ void diag_tile_fast(const DevBatch& db, int slot, int
     __syncthreads();
   }
   // ---- off-diagonal blocks of the inverse, by sub-diagonal s = i - j ----
-  for (int sd = 1; sd < ((db.ablate & 1024) ? 1 : 4); ++sd) {
+  for (int sd = 1; sd < 4; ++sd) {
     const int j = w, i = w + sd;
     if (i < 4) {
       // Y = sum_{k=j}^{i-1} L_ik X_kj
@@ -809,7 +688,7 @@ __device__ __forceinline__ void diag_tile_fast(const DevBatch& db, int slot, int
   }
   double* Li = db.Linv + (size_t)slot * db.mat + (size_t)jt * TS * ld + jt * TS;
   double* Mj = db.Mt + (size_t)slot * db.mat + (size_t)jt * TS * ld + jt * TS;
-  for (int e = tid; e < ((db.ablate & 2048) ? 0 : TS * TS); e += NTHR) {
+  for (int e = tid; e < TS * TS; e += NTHR) {
     const int r = e & 63, c = e >> 6;
     const double v = (r >= c) ? Xi[c * FS + r] : 0.0;
     Li[(size_t)c * ld + r] = v;                              // Linv[r][c]
@@ -818,143 +697,6 @@ __device__ __forceinline__ void diag_tile_fast(const DevBatch& db, int slot, int
   zp_diag(db, slot, jt, Xi, 1, FS, cbs);
 }
 
-
-// --------------------------------------------------------------------------------------------
-// Same leaf, ONE wave per slot (no workgroup barriers on the 128-step dependency chain).
-//   Cholesky: lane = row r; the row's not-yet-final columns sit in registers as chunks of 16,
-//     the current block's chunk first (chunks shift down after each block of 16 steps, so every
-//     register index is static).  Step k broadcasts the pivot a_kk by readlane, scales the column
-//     (l_rk = a_rk / l_kk), publishes it through LDS (col[k][r] = l_rk, 0 for r <= k) and updates
-//     a_rc -= l_rk l_ck for all remaining columns (zeros make c <= k a no-op).
-//   Inverse: lane = column c of X = L^-1, forward substitution by columns of L read back from
-//     the LDS image (x_k *= 1/l_kk ; x_r -= l_rk x_k), finished rows parked in an LDS tile T.
-//   Outputs from T: Mt (lanes = columns of Mt, contiguous) and Linv (lanes = rows).
-//   Pivot failure handled as in k_diag.  LDS: DWS doubles per wave.
-// --------------------------------------------------------------------------------------------
-constexpr int CS = 66;  // LDS row stride (16-B aligned rows)
-constexpr int DWS = 2 * TS * CS;
-// a[q][i] -= f * v[16q + i] for the NQ live chunks (static), 8 columns at a time
-template <int NQ>
-__device__ __forceinline__ void chunk_update(double (&a)[4][16], const double* v, double f) {
-#pragma unroll
-  for (int q = 0; q < NQ; ++q)
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      double2 b[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) b[i] = *(const double2*)(v + 16 * q + 8 * h + 2 * i);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        a[q][8 * h + 2 * i] = fma(-f, b[i].x, a[q][8 * h + 2 * i]);
-        a[q][8 * h + 2 * i + 1] = fma(-f, b[i].y, a[q][8 * h + 2 * i + 1]);
-      }
-    }
-}
-// 16 Cholesky steps of block kb (NQ = 4 - kb live chunks)
-template <int NQ>
-__device__ __forceinline__ void potrf_block(double (&a)[4][16], double* col, int kb, int r, int& fail) {
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const int k = 16 * kb + j;
-    const double ak = a[0][j];
-    const double p = readlane_d(ak, k);
-    const double pk = (p > 0.0) ? p : 1.0;
-    if (!(p > 0.0) && fail < 0) fail = k;
-    const double lkk = sqrt(pk), rk = recip(lkk);
-    const double l = (r > k) ? ak * rk : 0.0;
-    // column k of L below the diagonal; 1/l_kk parked on the diagonal (no lane branch: a
-    // branch here splits the block and lets the compiler sink the FMAs across steps)
-    col[k * CS + r] = (r == k) ? rk : l;
-    __builtin_amdgcn_wave_barrier();
-    chunk_update<NQ>(a, col + k * CS + 16 * kb, l);
-    // keep each step's reads and FMAs inside the step: otherwise the scheduler defers the FMAs
-    // of far columns behind the pivot chain and spills the early-issued LDS reads
-    __builtin_amdgcn_sched_barrier(0);
-  }
-}
-template <int NQ>
-__device__ __forceinline__ void trtri_block(double (&a)[4][16], const double* col, int kb) {
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const int k = 16 * kb + j;
-    const double* ck = col + k * CS;
-    const double xk = a[0][j] * ck[k];
-    chunk_update<NQ>(a, ck + 16 * kb, xk);  // l_rk for r > k, 0 for r < k (r = k: restored below)
-    a[0][j] = xk;
-    __builtin_amdgcn_sched_barrier(0);
-  }
-}
-__device__ __forceinline__ void chunk_shift(double (&a)[4][16]) {
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    a[0][i] = a[1][i];
-    a[1][i] = a[2][i];
-    a[2][i] = a[3][i];
-  }
-}
-__device__ __forceinline__ void diag_wave(const DevBatch& db, int slot, int jt, double* sm) {
-  const int r = threadIdx.x & 63;
-  const size_t ld = db.ld;
-  double* col = sm;               // [64][CS]: column k of L at col[k*CS + r]
-  double* T = sm + TS * CS;       // [64][CS]: X rows
-  const double* A = db.K + (size_t)slot * db.mat + (size_t)jt * TS * ld + jt * TS;
-  double a[4][16];
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) a[q][i] = A[(size_t)(16 * q + i) * ld + r];  // lower part used only
-  int fail = -1;
-  potrf_block<4>(a, col, 0, r, fail);
-  chunk_shift(a);
-  potrf_block<3>(a, col, 1, r, fail);
-  chunk_shift(a);
-  potrf_block<2>(a, col, 2, r, fail);
-  chunk_shift(a);
-  potrf_block<1>(a, col, 3, r, fail);
-  __builtin_amdgcn_wave_barrier();
-  {
-    const double s = -wave_sum(log(col[r * CS + r]));  // sum log l_kk = -sum log(1/l_kk)
-    if (r == 0) {
-      db.logdet_part[(size_t)slot * db.nt + jt] = s;
-      if (fail >= 0 && db.status[slot] == 0) {
-        db.status[slot] = 1;
-        db.info[slot] = jt * TS + fail + 1;
-      }
-    }
-  }
-  // X = L^-1, lane = column c
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) a[q][i] = (16 * q + i == r) ? 1.0 : 0.0;
-  trtri_block<4>(a, col, 0);
-#pragma unroll
-  for (int i = 0; i < 16; ++i) T[i * CS + r] = a[0][i];  // X[i][c], lane c
-  chunk_shift(a);
-  trtri_block<3>(a, col, 1);
-#pragma unroll
-  for (int i = 0; i < 16; ++i) T[(16 + i) * CS + r] = a[0][i];
-  chunk_shift(a);
-  trtri_block<2>(a, col, 2);
-#pragma unroll
-  for (int i = 0; i < 16; ++i) T[(32 + i) * CS + r] = a[0][i];
-  chunk_shift(a);
-  trtri_block<1>(a, col, 3);
-#pragma unroll
-  for (int i = 0; i < 16; ++i) T[(48 + i) * CS + r] = a[0][i];
-  __builtin_amdgcn_wave_barrier();
-  double* Mj = db.Mt + (size_t)slot * db.mat + (size_t)jt * TS * ld + jt * TS;
-  double* Li = db.Linv + (size_t)slot * db.mat + (size_t)jt * TS * ld + jt * TS;
-  for (int q = 0; q < TS; ++q) {
-    Mj[(size_t)q * ld + r] = T[q * CS + r];  // Mt[c=r][r'=q] = X[q][r]
-    Li[(size_t)q * ld + r] = T[r * CS + q];  // Linv[r][q]    = X[r][q]
-  }
-  zp_diag(db, slot, jt, T, CS, 1);
-}
-__global__ __launch_bounds__(64) void k_diag_w(DevBatch db, int jt) {
-  __shared__ __attribute__((aligned(16))) double sm[DWS];
-  diag_wave(db, blockIdx.x, jt, sm);
-}
 
 // ============================================================================================
 // Generic batched tile GEMM of the recursion (see GemmOp).  Unit = 2 x 2 output tiles; wave
@@ -1358,9 +1100,9 @@ __device__ __forceinline__ void leaf_body(const DevBatch& db, int o, int n) {
   const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
   for (int k = 0; k < n; ++k) {
     const int tk = o + k, m = n - 1 - k;
-    if (!(db.ablate & 8)) diag_tile_fast(db, slot, tk);  // ablate bits: timing experiments only
+    diag_tile_fast(db, slot, tk);
     __syncthreads();
-    for (int t = w; t < ((db.ablate & 16) ? 0 : m); t += 4) {  // TRSM: L[ti,tk] = K[ti,tk] Linv[tk,tk]^T
+    for (int t = w; t < m; t += 4) {  // TRSM: L[ti,tk] = K[ti,tk] Linv[tk,tk]^T
       const int ti = tk + 1 + t;
       d4 acc[QM][QN];
       acc4_zero(acc);
@@ -1368,7 +1110,7 @@ __device__ __forceinline__ void leaf_body(const DevBatch& db, int o, int n) {
       acc4_store(Lw + (size_t)(tk * TS) * ld + ti * TS, ld, acc, 1.0);
     }
     __syncthreads();
-    for (int t = w; t < ((db.ablate & 16) ? 0 : m * (m + 1) / 2); t += 4) {  // SYRK (lower trailing tiles)
+    for (int t = w; t < m * (m + 1) / 2; t += 4) {  // SYRK (lower trailing tiles)
       int a = t, c = 0;
       while (a >= m - c) {
         a -= m - c;
@@ -1390,7 +1132,7 @@ __device__ __forceinline__ void leaf_body(const DevBatch& db, int o, int n) {
   }
   // off-diagonal inverse tiles by sub-diagonal s:  X = sum_{k=tj}^{ti-1} L[ti,k] Linv[k,tj] (kept
   // transposed in Mt[tj,ti] as scratch), Linv[ti,tj] = -Linv[ti,ti] X; one wave per tile
-  for (int s = 1; s < ((db.ablate & 32) ? 0 : n); ++s) {
+  for (int s = 1; s < n; ++s) {
     for (int t = w; t < n - s; t += 4) {
       const int tj = o + t, ti = tj + s;
       double* Xt = Mt + (size_t)(ti * TS) * ld + tj * TS;  // Mt[tj,ti]
@@ -1541,7 +1283,7 @@ __device__ __forceinline__ void lauum_unit(const DevBatch& db, int slot, int pr,
   d4 acc[QM][QN];
   acc4_zero(acc);
   const size_t ld = db.ld, so = (size_t)slot * db.mat;
-  if (active && !(db.ablate & 1))
+  if (active)
     mma_64x64(acc, db.Mt + so + (size_t)ti * TS * ld + ti * TS, ld, db.Mt + so + (size_t)ti * TS * ld + tj * TS, ld,
               (nt - ti) * TS);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA landed
@@ -1562,7 +1304,7 @@ __device__ __forceinline__ void lauum_unit(const DevBatch& db, int slot, int pr,
     als[tid] = tile < nt ? al[tile * TS + pt] : 0.0;
   }
   __syncthreads();
-  if (active && !(db.ablate & 2)) {
+  if (active) {
     const double sf2 = P[d];
     const double* xr = xr_s + wr * xt;  // [r][xs]
     const double* xc = xc_s + wc * xt;  // [c][xs]
@@ -1605,7 +1347,7 @@ __device__ __forceinline__ void lauum_unit(const DevBatch& db, int slot, int pr,
               tr += W;
             } else {
               const double rr = fma(-2.0, cr[q], nr[r] + nc[c]);
-              const double kf = (db.ablate & 64) ? 1.0 : sf2 * exp_neg(-0.5 * (rr > 0.0 ? rr : 0.0));
+              const double kf = sf2 * exp_neg(-0.5 * (rr > 0.0 ? rr : 0.0));
               G = W * kf;
             }
             sf += G;
@@ -1639,7 +1381,7 @@ __device__ __forceinline__ void lauum_unit(const DevBatch& db, int slot, int pr,
         s += __shfl_xor(s, 8);
         Cs[b][q] = s;
       }
-    const int H = (db.ablate & 128) ? 0 : (d + 15) >> 4;
+    const int H = (d + 15) >> 4;
 #pragma unroll 1
     for (int h = 0; h < H; ++h) {
       // A operand: x of column point c = 16b + 4q + lk, dimension pA = 16h + lr
@@ -1706,11 +1448,7 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
   lauum_body(db);
 }
 int lauum_units(int nt) { return quad_units(nt, nt, true); }
-static bool lauum_fold() {
-  const char* e = getenv("GPRX_LAUUM_FOLD");  // experiment: 0 = one unit per workgroup
-  return !e || atoi(e) != 0;
-}
-int lauum_jobs(int nt) { return lauum_fold() ? (lauum_units(nt) + 1) / 2 : lauum_units(nt); }
+int lauum_jobs(int nt) { return (lauum_units(nt) + 1) / 2; }
 void lauum_order_host(int nt, int* out) {
   // 2 x 2-tile units of the lower triangle (first row, first column, unit id), K range [row, nt);
   // folded into jobs of two: the i-th longest with the i-th shortest (then the middle one alone),
@@ -2032,9 +1770,7 @@ __global__ __launch_bounds__(64) void k_params(DevBatch b) {
 void launch_params(const DevBatch& b, hipStream_t s) { hipLaunchKernelGGL(k_params, dim3((b.B + 63) / 64), dim3(64), 0, s, b); }
 void launch_center(const DevBatch& b, hipStream_t s) { hipLaunchKernelGGL(k_center, dim3(b.B), dim3(NTHR), 0, s, b); }
 void launch_diag(const DevBatch& b, int jt, hipStream_t s) {
-  if (b.diag_variant == 1) hipLaunchKernelGGL(k_diag_w, dim3(b.B), dim3(64), 0, s, b, jt);
-  else if (b.diag_variant == 2) hipLaunchKernelGGL(k_diag_f, dim3(b.B), dim3(NTHR), 0, s, b, jt);
-  else hipLaunchKernelGGL(k_diag, dim3(b.B), dim3(NTHR), 0, s, b, jt);
+  hipLaunchKernelGGL(k_diag_f, dim3(b.B), dim3(NTHR), 0, s, b, jt);
 }
 void launch_leaf(const DevBatch& b, int o, int n, hipStream_t s) {
   hipLaunchKernelGGL(k_leaf, dim3(b.B), dim3(NTHR), 0, s, b, o, n);

@@ -356,12 +356,17 @@ __global__ __launch_bounds__(64) void k_lbfgs(LbArgs a, DevBatch db, int init) {
   ri[3] = I[I_STOP] | (I[I_CONV] ? 0x100 : 0);
 }
 
-// the minimiser's kernel parameters (Optim's result -> set_params!; update_target! follows)
+// the minimiser's kernel parameters (Optim's result -> set_params!; update_target! follows).  The
+// minimiser is written as it is: a non-finite one (the NaN-gradient stop of a non-PD start) makes
+// derive_params mark the slot GPRX_INVALID_ARGUMENT, so the refit reports it instead of quietly
+// factorising the start point.
 __global__ __launch_bounds__(64) void k_lbfgs_final(LbArgs a, DevBatch db) {
   const int slot = blockIdx.x * 64 + threadIdx.x;
   if (slot >= db.B) return;
   LbView v = lb_view(a, slot);
-  lb_write_params(a, db, slot, v.x, v.th0);
+  double* T = db.theta + (size_t)slot * a.n;
+  for (int q = 0; q < a.n; ++q) T[q] = v.x[q];
+  derive_params(db, slot);
 }
 
 void launch_lbfgs(const LbArgs& a, const DevBatch& db, int init, hipStream_t s) {

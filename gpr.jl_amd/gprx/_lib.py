@@ -28,6 +28,10 @@ DIST_DIRECT = 1
 MEM_HOST = 0
 MEM_DEVICE = 1
 
+OPT_LEAF_TILES = 1
+OPT_SMALL_N = 2
+OPT_GRAPHS = 3
+
 STOP_NAMES = {0: "iterations", 1: "g_tol", 2: "x_tol", 3: "f_tol", 4: "linesearch", 5: "max_evals", 6: "time_limit",
               7: "nan_gradient"}
 STOP_CONVERGED = 0x100
@@ -55,6 +59,7 @@ SIGNATURES = {
     "gprx_ctx_set_dist_mode": (C.c_int, [_vp, C.c_int]),
     "gprx_ctx_device": (C.c_int, [_vp]),
     "gprx_ctx_set_profiling": (C.c_int, [_vp, C.c_int]),
+    "gprx_ctx_set_option": (C.c_int, [_vp, C.c_int, C.c_int]),
     "gprx_ctx_kernel_stats": (C.c_int, [_vp, C.c_char_p, _dp, C.POINTER(C.c_int64), _dp, _dp]),
     "gprx_ctx_reset_stats": (C.c_int, [_vp]),
     "gprx_batch_create": (C.c_int, [_vp, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(_vp)]),
@@ -64,6 +69,7 @@ SIGNATURES = {
     "gprx_batch_run": (C.c_int, [_vp, _dp, C.c_uint, _dp, _dp, _dp, _dp, _ip, _ip]),
     "gprx_batch_predict": (C.c_int, [_vp, _dp, _dp]),
     "gprx_batch_dims": (C.c_int, [_vp, _ip, _ip, _ip, _ip]),
+    "gprx_batch_alpha": (C.c_int, [_vp, _dp]),
     "gprx_opt_defaults": (None, [C.POINTER(OptOptions)]),
     "gprx_batch_optimize": (C.c_int, [_vp, _dp, C.POINTER(OptOptions), _dp, _dp, _ip, _ip, _ip, _ip, _ip]),
     "gprx_gp_create": (C.c_int, [_vp, _dp, C.c_int, C.c_int, _dp, C.POINTER(_vp)]),

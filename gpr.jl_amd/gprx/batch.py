@@ -46,6 +46,11 @@ class Context:
         L.check(L.lib.gprx_ctx_set_dist_mode(self.h, int(mode)), self.h)
         self.dist_mode = int(mode)
 
+    def set_option(self, option: int, value: int):
+        """Launch-geometry option (gprx_ctx_set_option: L.OPT_LEAF_TILES / OPT_SMALL_N / OPT_GRAPHS);
+        results are identical under every setting."""
+        L.check(L.lib.gprx_ctx_set_option(self.h, int(option), int(value)), self.h)
+
     def set_profiling(self, enable: bool):
         L.check(L.lib.gprx_ctx_set_profiling(self.h, 1 if enable else 0), self.h)
 
@@ -173,7 +178,9 @@ class GPBatch:
         every slot (CPnoise.jl:41), on the device (k_lbfgs: gprx/optim.py's algorithm as a per-slot
         state machine, lock-step over the batch).  method / options: gprx.optim.LBFGS / Options.
         Returns (results, rounds) like gprx.optim.optimize_batch; with refit the batch ends
-        factorised at the minimisers (optimize!'s update_target!), so predict() uses them."""
+        factorised at the minimisers (optimize!'s update_target!), so predict() uses them.  A
+        minimiser whose refit fails raises (update_target!'s PosDefException / ArgumentError) with
+        the results attached as `err.results`; the batch is then left unfactorised."""
         from .optim import LBFGS, Options, Result
 
         method = method or LBFGS()
@@ -199,10 +206,18 @@ class GPBatch:
         fmin = np.empty(B)
         its, fc, gc, stp = (np.empty(B, dtype=np.int32) for _ in range(4))
         rounds = C.c_int(0)
-        L.check(L.lib.gprx_batch_optimize(self.h, L.dptr(theta0), C.byref(o), L.dptr(th), L.dptr(fmin), L.iptr(its),
-                                          L.iptr(fc), L.iptr(gc), L.iptr(stp), C.byref(rounds)), self.ctx.h)
+        rc = L.lib.gprx_batch_optimize(self.h, L.dptr(theta0), C.byref(o), L.dptr(th), L.dptr(fmin), L.iptr(its),
+                                       L.iptr(fc), L.iptr(gc), L.iptr(stp), C.byref(rounds))
+        if rc not in (L.OK, L.NOT_POSITIVE_DEFINITE, L.INVALID_ARGUMENT):
+            L.check(rc, self.ctx.h)
         res = [Result(th[s].copy(), float(fmin[s]), int(its[s]), int(fc[s]), int(gc[s]),
                       bool(stp[s] & L.STOP_CONVERGED), L.STOP_NAMES[int(stp[s]) & 0xFF]) for s in range(B)]
+        if rc != L.OK:  # the refit at a minimiser failed: the search results are still valid
+            try:
+                L.check(rc, self.ctx.h)
+            except L.GPRXError as e:
+                e.results = (res, int(rounds.value))
+                raise
         return res, int(rounds.value)
 
     def predict(self, variance: bool = True):
@@ -212,6 +227,12 @@ class GPBatch:
         var = np.empty((self.B, self.M)) if variance else None
         L.check(L.lib.gprx_batch_predict(self.h, L.dptr(mu), L.dptr(var)), self.ctx.h)
         return mu, var
+
+    def alpha(self):
+        """alpha = K^-1 (y - mean) per slot from the last successful factorisation (gp.alpha)."""
+        out = np.empty((self.B, self.N))
+        L.check(L.lib.gprx_batch_alpha(self.h, L.dptr(out)), self.ctx.h)
+        return out
 
     def close(self):
         if getattr(self, "h", None):

@@ -70,30 +70,54 @@ end
 # θ in GaussianProcesses' optimiser order: [logNoise; mean params (none); logℓ...; logσ]
 theta(gp::GPE) = Float64[gp.logNoise.value; GaussianProcesses.get_params(gp.kernel)...]
 
-function check(rc::Cint, gp)
-    rc == NOT_PD && throw(LinearAlgebra.PosDefException(-1))
+# status -> the exception GaussianProcesses' own path raises; `info` is the 1-based failing pivot
+# the ABI reports (LAPACK dpotrf's info, as cholesky! puts it into PosDefException)
+function check(rc::Cint, gp, info::Integer=-1)
+    rc == NOT_PD && throw(LinearAlgebra.PosDefException(Int(info)))
     rc == INVALID && throw(ArgumentError("gprx: invalid hyperparameters"))
     rc == OK || error("gprx device error ($rc)")
+end
+
+# One evaluation of the GP's batch of one (gprx_batch_run: it also reports the failing pivot).
+# flags: 1 = gradient.  Afterwards gp.alpha holds K^-1 (y - m(X)) of the device factorisation.
+function evaluate!(gp::GPE, flags::Integer)
+    b = ccall((:gprx_gp_batch, LIB), Ptr{Cvoid}, (Ptr{Cvoid},), handle(gp).ptr)
+    m = Ref{Float64}(0.0)
+    g = zeros(length(theta(gp)))
+    st, info = Ref{Cint}(0), Ref{Cint}(0)
+    rc = ccall((:gprx_batch_run, LIB), Cint,
+               (Ptr{Cvoid}, Ptr{Float64}, Cuint, Ref{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
+                Ref{Cint}, Ref{Cint}),
+               b, theta(gp), Cuint(flags), m, g, C_NULL, C_NULL, st, info)
+    check(rc, gp, info[])
+    a = zeros(length(gp.y))
+    check(ccall((:gprx_batch_alpha, LIB), Cint, (Ptr{Cvoid}, Ptr{Float64}), b, a), gp)
+    gp.alpha = a
+    return m[], g
+end
+
+# gp.cK (the host PDMat of K and its Cholesky factor) is not maintained by the device path: the
+# factorisation stays in HBM.  Code that reads it (full-covariance prediction, rand, ...) calls
+# materialize!(gp) first, which runs GaussianProcesses' own update_cK! / update_mll! on the host
+# once at the current hyperparameters (O(N^3) on the CPU, on request only).
+function materialize!(gp::GPE)
+    invoke(GaussianProcesses.update_mll!, Tuple{GPE}, gp)
+    gp
 end
 
 # The varargs absorb GaussianProcesses' optional positional arguments (e.g. the precompute buffer
 # that optimize! passes to update_target_and_dtarget!) so these methods win dispatch for every
 # call form.
 function GaussianProcesses.update_mll!(gp::GPE{<:Any,<:Any,<:Mean,<:SEArd}, args...; kwargs...)
-    m = Ref{Float64}(0.0)
-    check(ccall((:gprx_gp_lml, LIB), Cint, (Ptr{Cvoid}, Ptr{Float64}, Ref{Float64}),
-                handle(gp).ptr, theta(gp), m), gp)
-    gp.mll = m[]
+    m, _ = evaluate!(gp, 0)
+    gp.mll = m
     gp.target = gp.mll
     gp
 end
 
 function GaussianProcesses.update_target_and_dtarget!(gp::GPE{<:Any,<:Any,<:Mean,<:SEArd}, args...; kwargs...)
-    m = Ref{Float64}(0.0)
-    g = zeros(length(theta(gp)))
-    check(ccall((:gprx_gp_lml_grad, LIB), Cint, (Ptr{Cvoid}, Ptr{Float64}, Ref{Float64}, Ptr{Float64}),
-                handle(gp).ptr, theta(gp), m, g), gp)
-    gp.mll = m[]
+    m, g = evaluate!(gp, 1)
+    gp.mll = m
     gp.dmll = g
     gp.target = gp.mll
     gp.dtarget = g
@@ -101,7 +125,10 @@ function GaussianProcesses.update_target_and_dtarget!(gp::GPE{<:Any,<:Any,<:Mean
 end
 
 function GaussianProcesses.predict_f(gp::GPE{<:Any,<:Any,<:Mean,<:SEArd}, x::AbstractMatrix; full_cov::Bool=false)
-    full_cov && error("gprx: full_cov=true is not provided by the device path")
+    if full_cov  # the M x M posterior covariance: GaussianProcesses' own host method on gp.cK
+        materialize!(gp)
+        return invoke(GaussianProcesses.predict_f, Tuple{GPE,AbstractMatrix}, gp, x; full_cov=true)
+    end
     xs = Matrix{Float64}(x)
     M = size(xs, 2)
     mu = zeros(M)

@@ -83,6 +83,15 @@ int gprx_ctx_set_dist_mode(gprx_ctx* ctx, int mode);
 int gprx_ctx_device(const gprx_ctx* ctx);
 /* per-kernel timing (HIP events around every launch on the context stream); off by default */
 int gprx_ctx_set_profiling(gprx_ctx* ctx, int enable);
+/* launch-geometry options (results are identical under every setting; tests cover each path):
+ *   GPRX_OPT_LEAF_TILES  recursion nodes of <= value tiles (64 x 64) run fused in one leaf
+ *                        kernel; 1: every 64 x 64 diagonal tile on its own; 0 (default) = auto
+ *   GPRX_OPT_SMALL_N     recursion nodes of <= value tiles use the 64 x 32 pair-unit GEMM; 0 = auto
+ *   GPRX_OPT_GRAPHS      1: replay each evaluation's launch sequence as a hipGraph (default 0)  */
+#define GPRX_OPT_LEAF_TILES 1
+#define GPRX_OPT_SMALL_N 2
+#define GPRX_OPT_GRAPHS 3
+int gprx_ctx_set_option(gprx_ctx* ctx, int option, int value);
 int gprx_ctx_kernel_stats(gprx_ctx* ctx, const char* kernel, double* total_ms, int64_t* launches,
                           double* algo_flops, double* algo_bytes);
 int gprx_ctx_reset_stats(gprx_ctx* ctx);
@@ -111,6 +120,9 @@ int gprx_batch_run(gprx_batch* batch, const double* theta, unsigned flags, doubl
  * var == NULL: mean only.                                                                      */
 int gprx_batch_predict(gprx_batch* batch, double* mu, double* var);
 int gprx_batch_dims(const gprx_batch* batch, int* B, int* d, int* N, int* M_max);
+/* alpha = K^-1 (y - mean) of the last successful factorisation, alpha[b*N + t] (GPE's gp.alpha;
+ * N doubles per slot), for hosts that keep GaussianProcesses' own fields current.              */
+int gprx_batch_alpha(gprx_batch* batch, double* alpha);
 
 /* ---- hyper-parameter optimisation on the device ------------------------------------------- */
 /* GaussianProcesses.optimize!(gp, LBFGS(linesearch=BackTracking(order=2)), Optim.Options(...))
@@ -149,7 +161,13 @@ void gprx_opt_defaults(gprx_opt_options* opt);
  * minimum[B] = -mll at the minimiser as Optim reports it, iterations/f_calls/g_calls[B],
  * stopped[B] = GPRX_STOP_* | GPRX_STOP_CONVERGED, rounds = batch evaluations performed
  * (excluding the refit).  Returns GPRX_OK, or an error of the evaluations themselves
- * (device / memory); per-slot failures are +Inf answers, not errors.                          */
+ * (device / memory); per-slot failures during the search are +Inf answers, not errors.  With
+ * refit, a minimiser whose refit fails (not finite: GPRX_INVALID_ARGUMENT; not positive definite:
+ * GPRX_NOT_POSITIVE_DEFINITE) is returned as that status (first failing slot), the outputs are
+ * still filled, and the batch is left unfactorised (predict answers GPRX_NOT_READY).
+ * time_limit is one wall clock for the whole call (all slots), not per GP as Optim's per-call
+ * Options(time_limit=10.) at CPnoise.jl:41.  The context's mutex is held for the whole call:
+ * other threads sharing the context wait until the optimisation ends.                         */
 int gprx_batch_optimize(gprx_batch* batch, const double* theta0, const gprx_opt_options* opt, double* theta_out,
                         double* minimum, int* iterations, int* f_calls, int* g_calls, int* stopped, int* rounds);
 

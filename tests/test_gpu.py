@@ -242,15 +242,15 @@ def test_optimize_batch_matches_single_gp_runs(gprx, ctx, golden_dir):
         assert res[s].minimum == ref.minimum
 
 
-def test_graph_replay_matches_direct_launches(gprx, golden_dir, monkeypatch):
+def test_graph_replay_matches_direct_launches(gprx, golden_dir):
     """The hipGraph replay (default) and direct stream launches give bit-identical results,
     including after the test set (and so the captured geometry) changes."""
     z = np.load(golden_dir / "p2_n256.npz")
     X, Y, th, Xs = z["X"], z["Y"], z["theta"], z["Xs"]
     out = []
-    for graphs in ("1", "0"):
-        monkeypatch.setenv("GPRX_GRAPHS", graphs)
+    for graphs in (1, 0):
         c = gprx.Context(0)
+        c.set_option(gprx.OPT_GRAPHS, graphs)
         b = gprx.GPBatch(Y.shape[0], X.shape[0], X.shape[1], Xs.shape[1], ctx=c)
         b.set_train(X, Y)
         b.set_test(Xs)
@@ -266,14 +266,15 @@ def test_graph_replay_matches_direct_launches(gprx, golden_dir, monkeypatch):
     np.testing.assert_array_equal(out[0][1]["mu"], out[0][0]["mu"][:, :7])
 
 
-@pytest.mark.parametrize("leaf,diagv", [(1, 0), (1, 1), (1, 2), (2, 1), (4, 1), (8, 1)])
-def test_factorisation_paths_match_golden(gprx, golden_dir, monkeypatch, leaf, diagv):
-    """Every recursion leaf (fused k_leaf for 2..8 tiles, standalone 64x64 diagonal kernels
-    k_diag / k_diag_w / k_diag_f at leaf 1) gives the golden results, at N=256 (4 tiles) and
-    N=130 (ragged), and reports the same failing pivot on a non-PD slot."""
-    monkeypatch.setenv("GPRX_LEAF", str(leaf))
-    monkeypatch.setenv("GPRX_DIAGV", str(diagv))
+@pytest.mark.parametrize("leaf,small_n", [(1, 0), (2, 0), (4, 0), (8, 0), (1, 1), (4, 64)])
+def test_factorisation_paths_match_golden(gprx, golden_dir, leaf, small_n):
+    """Every recursion leaf (fused k_leaf for 2..8 tiles, the standalone 64x64 diagonal kernel at
+    leaf 1) and both GEMM unit shapes (64 x 32 pair units below small_n tiles, 64 x 64 above)
+    give the golden results, at N=256 (4 tiles) and N=130 (ragged), and report the same failing
+    pivot on a non-PD slot."""
     c = gprx.Context(0)
+    c.set_option(gprx.OPT_LEAF_TILES, leaf)
+    c.set_option(gprx.OPT_SMALL_N, small_n)
     try:
         z = np.load(golden_dir / "p2_n256.npz")
         X, Y, th, Xs = z["X"], z["Y"], z["theta"], z["Xs"]
@@ -574,3 +575,53 @@ def test_device_optimize_failed_start_and_time_limit(gprx, ctx, golden_dir):
     assert dev[1].stopped_by == "max_evals"
     dev, _ = b.optimize(np.stack([good, good]), LBFGS(), Options(time_limit=0.0), refit=False)
     assert all(r.stopped_by == "time_limit" and r.iterations == 1 for r in dev)
+
+
+def test_device_optimize_refit_failure_is_reported(gprx, ctx, golden_dir):
+    """optimize! with the closing refit (update_target!) on a slot whose search ended at a
+    non-finite minimiser (the NaN-gradient stop of a non-PD start): the call reports the refit's
+    failure (first failing slot) with the search results attached, and the batch is left
+    unfactorised, so predict() answers NOT_READY instead of values for the wrong theta."""
+    from gprx.optim import LBFGS, Options
+
+    z = np.load(golden_dir / "nonpd_p1.npz")
+    X, Y, th = z["X"], z["Y"], z["theta"]
+    good = th.copy()
+    good[0] = -2.0
+    b = gprx.GPBatch(2, X.shape[0], X.shape[1], 4, ctx=ctx)
+    b.set_train(X, Y[:2])
+    b.set_test(X[:, :4])
+    b.run(np.stack([good, good]))  # factorised before the call
+    with pytest.raises(gprx.GPRXError) as e:
+        b.optimize(np.stack([th, good]), LBFGS(), Options(max_evals=80), refit=True)
+    assert e.value.status in (1, 2)
+    res, _ = e.value.results
+    assert res[0].stopped_by == "nan_gradient" and res[1].stopped_by in ("max_evals", "g_tol", "f_tol", "x_tol")
+    with pytest.raises(gprx.GPRXError) as e2:
+        b.predict()
+    assert e2.value.status == 5  # GPRX_NOT_READY
+    # a healthy batch refits and predicts as before
+    res2, _ = b.optimize(np.stack([good, good]), LBFGS(), Options(max_evals=10), refit=True)
+    mu, var = b.predict()
+    r = b.run(np.stack([x.minimizer for x in res2]), grad=False, predict=True)
+    np.testing.assert_array_equal(mu, r["mu"])
+    b.close()
+
+
+def test_alpha_export_matches_oracle(gprx, ctx, golden_dir):
+    """gprx_batch_alpha (gp.alpha for hosts that keep GaussianProcesses' fields current) equals
+    the oracle's alpha = K^-1 y; before any factorisation it answers NOT_READY."""
+    z = np.load(golden_dir / "p2_n100.npz")
+    X, Y, th = z["X"], z["Y"], z["theta"]
+    G = Y.shape[0]
+    b = gprx.GPBatch(G, X.shape[0], X.shape[1], 0, ctx=ctx)
+    b.set_train(X, Y)
+    with pytest.raises(gprx.GPRXError) as e:
+        b.alpha()
+    assert e.value.status == 5
+    b.run(np.tile(th, (G, 1)))
+    a = b.alpha()
+    for g in range(G):
+        f = O.fit(X, Y[g], th, None, ctx.dist_mode)
+        np.testing.assert_allclose(a[g], f["alpha"], rtol=0, atol=1e-9 * np.max(np.abs(f["alpha"])))
+    b.close()
