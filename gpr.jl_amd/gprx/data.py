@@ -230,3 +230,38 @@ def theta0_min(mech: str, key_n: int, usesin: bool = False) -> np.ndarray:
         lq, lv = p[1 + 2 * c], p[2 + 2 * c]
         ell += [lq, lq, lv] if (usesin and ang) else [lq, lv]
     return theta_from_params(np.concatenate([[p[0]], ell]))
+
+
+# ---- ground truth of the sweep's test rollouts ----------------------------------------------
+def test_truth(mech: str, M: int, seed: int, steps: int) -> dict:
+    """The noise-free test states of make_trial / make_trial_min (the same draws from the test
+    generator, before the noise the experiments add to testdf: CPnoise.jl:21-24) advanced by the
+    generator's own dynamics over steps + 1 mechanism steps -- the rollout's final time: the
+    minimal-coordinate loop first moves q by qdot*dt, then takes `steps` predicted steps
+    (predictdynamics.jl:41-46); the maximal-coordinate loop takes `steps` predicted steps and one
+    closing updatestate! (:11-21).  Plays the role of testdf.sfuture (xtest_future_true, :17).
+    Returns q (M, 2nc) minimal coordinates and X (d, M) CStates of the final states."""
+    rng_t = np.random.default_rng(seed + 500000)
+    m = _sample_minimal(mech, M, rng_t)
+    for _ in range(steps + 1):
+        m = _step(mech, m)
+    keys = MIN_COORDS[mech]
+    q = np.stack([m[k] for pair in keys for k in pair], axis=1)
+    return dict(q=q, X=_cstates(mech, m))
+
+
+def position_mse(truth: np.ndarray, pred: np.ndarray) -> float:
+    """simulationerror(groundtruth, predictions) (examples/utils/utils.jl:36-46): squared position
+    error over every body of every test sample / (3 Nbodies M); NaN -> Inf.  truth, pred: (M, d)
+    CStates."""
+    truth = np.asarray(truth, dtype=np.float64)
+    pred = np.asarray(pred, dtype=np.float64)
+    M, d = truth.shape
+    nb = d // 13
+    err = 0.0
+    for i in range(M):
+        for b in range(nb):
+            o = 13 * b
+            err += float(np.sum((truth[i, o:o + 3] - pred[i, o:o + 3]) ** 2))
+    err /= 3 * nb * M
+    return math.inf if math.isnan(err) else err

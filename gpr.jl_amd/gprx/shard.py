@@ -6,17 +6,23 @@ per-output GPs share X but are independent (examples/maximal_coordinates/CPnoise
 Here one process drives one GPU (torch.distributed; backend "nccl" = RCCL over xGMI on ROCm,
 "gloo" for the CPU tests) and the unit of work is a (trial, output) pair:
 
-  * trial-major round robin: whole trials go to ranks, so a trial's X is uploaded once per GPU
-    and no data moves between GPUs during a fit (`shard_trials`);
+  * trial-major round robin: whole trials go to ranks (`shard_trials`), and each rank evaluates
+    ALL of its trials x G outputs as ONE device batch (`RankBatch`: B = local trials x G slots,
+    built once, reused for every evaluation and optimiser round) -- the batching the bench
+    measures, instead of one small launch sequence per trial;
+  * no data moves between GPUs during a fit; trial inputs are generated (or loaded) on the rank
+    that owns them;
   * when a single trial must be spread (G outputs over several GPUs, e.g. one P2 trial on 8
-    GPUs), the owning rank broadcasts X, Y, theta once (`broadcast_trial`, ≤ 1.7 MB) and every
-    rank evaluates its outputs k ≡ rank (mod world);
-  * results (mll, gradient, predictive mean / variance: a few KB) are gathered to rank 0
-    (`gather_results`).
+    GPUs), the owning rank broadcasts X, Y, theta once (`broadcast_trial`, <= 1.7 MB) and every
+    rank evaluates its outputs k = rank (mod world) (`run_trial_split`);
+  * results (mll, gradient, theta*, predictive mean / variance, status: a few KB per trial) are
+    gathered as raw fp64 tensors with one all_gather per array (`gather_rows`), over RCCL when
+    the group is nccl.
 
-There is no all-reduce on the hot path.  The per-rank evaluator is injected (`evaluate(X, Y,
-theta, Xs) -> dict`), so the host logic is testable on CPU with gloo; the product evaluator is
-`gpu_evaluator()` (GPBatch on the rank's MI355X).
+There is no all-reduce on the data path.  The per-rank evaluator is injected
+(`evaluate(local_trials) -> dict of (n_local, G, ...) arrays`), so the host logic is testable on
+CPU with gloo and the oracle; the product evaluator is `RankBatch` (one GPBatch on the rank's
+MI355X).
 """
 from __future__ import annotations
 
@@ -34,38 +40,159 @@ def shard_outputs(G: int, rank: int, world: int) -> list[int]:
     return list(range(rank, G, world))
 
 
-def gpu_evaluator(device: int | None = None, ctx=None):
-    """Evaluator running on this rank's GPU: one GPBatch per call (B = number of GPs)."""
-    from .batch import GPBatch, Context
-
-    if ctx is None:
-        import torch
-
-        ctx = Context(torch.cuda.current_device() if device is None else device)
-
-    def evaluate(X, Y, theta, Xs=None):
-        X = np.asarray(X, dtype=np.float64)
-        Y = np.atleast_2d(np.asarray(Y, dtype=np.float64))
-        theta = np.atleast_2d(np.asarray(theta, dtype=np.float64))
-        B = Y.shape[0]
-        d, N = X.shape[-2], X.shape[-1]
-        M = 0 if Xs is None else np.asarray(Xs).shape[-1]
-        b = GPBatch(B, d, N, M, ctx=ctx)
-        try:
-            b.set_train(X, Y)
-            if M:
-                b.set_test(Xs)
-            return b.run(theta, grad=True, predict=M > 0)
-        finally:
-            b.close()
-
-    return evaluate
-
-
 def _dist():
     import torch.distributed as dist
 
     return dist
+
+
+def _device(dev=None):
+    dist = _dist()
+    if dev is not None:
+        return dev
+    return "cuda" if dist.get_backend() == "nccl" else "cpu"
+
+
+# ---- the product evaluator: one device batch per rank ----------------------------------------
+class RankBatch:
+    """All of a rank's trials x G outputs as one GPBatch (B = n_local * G slots, slot t*G + g =
+    local trial t, output g), built once and reused.  Each trial's X / Xs is the slot's own input
+    (trials differ), the G outputs of a trial share it.
+
+    trials: list of dicts X (d, N), Y (G, N) (targets minus prior mean), Xs (d, M) or None."""
+
+    def __init__(self, trials: Sequence[dict], ctx=None, device: int | None = None):
+        from .batch import Context, GPBatch
+
+        if ctx is None:
+            import torch
+
+            ctx = Context(torch.cuda.current_device() if device is None else device)
+        self.ctx = ctx
+        self.n = len(trials)
+        if self.n == 0:
+            self.batch = None
+            return
+        X0 = np.asarray(trials[0]["X"])
+        self.d, self.N = X0.shape
+        self.G = np.atleast_2d(trials[0]["Y"]).shape[0]
+        xs0 = trials[0].get("Xs")
+        self.M = 0 if xs0 is None else np.asarray(xs0).shape[1]
+        B = self.n * self.G
+        self.batch = GPBatch(B, self.d, self.N, self.M, ctx=ctx)
+        X = np.repeat(np.stack([np.asarray(t["X"], dtype=np.float64) for t in trials]), self.G, axis=0)
+        Y = np.concatenate([np.atleast_2d(np.asarray(t["Y"], dtype=np.float64)) for t in trials], axis=0)
+        self.batch.set_train(X, Y)
+        if self.M:
+            Xs = np.repeat(np.stack([np.asarray(t["Xs"], dtype=np.float64) for t in trials]), self.G, axis=0)
+            self.batch.set_test(Xs)
+
+    def _shape(self, a):
+        return None if a is None else np.asarray(a).reshape((self.n, self.G) + np.asarray(a).shape[1:])
+
+    def evaluate(self, theta, grad: bool = True, predict: bool | None = None, variance: bool = True) -> dict:
+        """theta (n_local, G, d+2) -> dict of (n_local, G, ...) arrays (mll, grad, mu, var, status,
+        info)."""
+        if self.batch is None:
+            return {}
+        th = np.asarray(theta, dtype=np.float64).reshape(self.n * self.G, -1)
+        pred = self.M > 0 if predict is None else predict
+        r = self.batch.run(th, grad=grad, predict=pred, variance=variance)
+        return {k: self._shape(v) for k, v in r.items() if v is not None}
+
+    def optimize(self, theta0, method=None, options=None) -> dict:
+        """optimize! for every GP of every local trial in one device call (k_lbfgs, lock-step),
+        then one evaluation at the minimisers (update_target!, with prediction when the trials
+        have test points).  A slot whose refit fails is reported in `status` (the reference's
+        experiment throws and the trial is dropped, core.jl:41-46), the others stay valid."""
+        if self.batch is None:
+            return {}
+        th0 = np.asarray(theta0, dtype=np.float64).reshape(self.n * self.G, -1)
+        res, rounds = self.batch.optimize(th0, method, options, refit=False)
+        thmin = np.stack([r.minimizer for r in res])
+        ok = np.all(np.isfinite(thmin), axis=1)
+        # a non-finite minimiser (NaN-gradient stop) is evaluated at its start and marked failed
+        r = self.batch.run(np.where(ok[:, None], thmin, th0), grad=False, predict=self.M > 0, variance=False)
+        status = np.where(ok, r["status"], 2).astype(np.int32)
+        out = {"theta": thmin, "minimum": np.array([x.minimum for x in res]), "mll": r["mll"], "status": status,
+               "f_calls": np.array([x.f_calls for x in res], dtype=np.int32),
+               "iterations": np.array([x.iterations for x in res], dtype=np.int32)}
+        if r.get("mu") is not None:
+            out["mu"] = r["mu"]
+        out = {k: self._shape(v) for k, v in out.items()}
+        out["rounds"] = rounds
+        return out
+
+    def slot(self, t: int, g: int) -> int:
+        return t * self.G + g
+
+    def close(self):
+        if self.batch is not None:
+            self.batch.close()
+            self.batch = None
+
+
+def gpu_evaluator(device: int | None = None, ctx=None):
+    """Evaluator for run_trials_sharded on this rank's GPU: one RankBatch over all local trials
+    (theta taken from each trial dict).  Callers that evaluate the same trials repeatedly (an
+    optimiser, a sweep) keep a RankBatch themselves and call its evaluate / optimize."""
+
+    def evaluate(trials):
+        rb = RankBatch(trials, ctx=ctx, device=device)
+        try:
+            return rb.evaluate(np.stack([np.atleast_2d(t["theta"]) for t in trials]))
+        finally:
+            rb.close()
+
+    return evaluate
+
+
+# ---- collectives: raw fp64 tensors ----------------------------------------------------------
+def gather_rows(local: np.ndarray, counts: Sequence[int], device=None) -> list[np.ndarray]:
+    """All-gather of per-rank row blocks (rank r holds counts[r] rows of equal trailing shape):
+    one fixed-size fp64 tensor per rank (padded to max(counts) rows), one all_gather.  Returns the
+    list of every rank's rows (on every rank)."""
+    import torch
+
+    dist = _dist()
+    dev = _device(device)
+    world = dist.get_world_size()
+    local = np.asarray(local, dtype=np.float64)
+    tail = local.shape[1:]
+    width = int(np.prod(tail)) if tail else 1
+    nmax = max(max(counts), 1)
+    buf = torch.zeros((nmax, width), dtype=torch.float64, device=dev)
+    if local.shape[0]:
+        buf[: local.shape[0]] = torch.from_numpy(np.ascontiguousarray(local.reshape(local.shape[0], width))).to(dev)
+    outs = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(outs, buf)
+    return [o[: counts[r]].cpu().numpy().reshape((counts[r],) + tail) for r, o in enumerate(outs)]
+
+
+def gather_results(local: dict, n_total: int, index_of_rank: Callable[[int], Sequence[int]], dst: int | None = 0,
+                   keys: Sequence[str] = ("mll", "grad", "mu", "var", "status", "info", "theta", "minimum")):
+    """Gather per-unit result arrays (first axis = local units, in the order index_of_rank(rank)
+    lists them) from every rank into global order.  Every key must be present on every rank with
+    the same trailing shape (a rank with no units sends zero rows).  Integer arrays travel as fp64
+    (exact).  Returns the assembled dict on dst (on every rank when dst is None), else None."""
+    dist = _dist()
+    rank, world = dist.get_rank(), dist.get_world_size()
+    idx = [list(index_of_rank(r)) for r in range(world)]
+    counts = [len(i) for i in idx]
+    out: dict = {}
+    for k in keys:
+        if k not in local:
+            continue
+        v = np.asarray(local[k])
+        parts = gather_rows(v.astype(np.float64), counts)
+        full = np.zeros((n_total,) + v.shape[1:], dtype=np.float64)
+        for r in range(world):
+            if counts[r]:
+                full[idx[r]] = parts[r]
+        out[k] = full.astype(v.dtype) if np.issubdtype(v.dtype, np.integer) else full
+    if dst is not None and rank != dst:
+        return None
+    return out
 
 
 def broadcast_trial(X, Y, theta, Xs=None, src: int = 0, device=None):
@@ -75,7 +202,7 @@ def broadcast_trial(X, Y, theta, Xs=None, src: int = 0, device=None):
 
     dist = _dist()
     rank = dist.get_rank()
-    dev = device if device is not None else ("cuda" if dist.get_backend() == "nccl" else "cpu")
+    dev = _device(device)
     meta = torch.zeros(5, dtype=torch.int64, device=dev)
     if rank == src:
         X = np.asarray(X, dtype=np.float64)
@@ -100,66 +227,65 @@ def broadcast_trial(X, Y, theta, Xs=None, src: int = 0, device=None):
     return X, Y, theta, Xs
 
 
-def gather_results(local: dict, n_total: int, index: Sequence[int], dst: int = 0):
-    """Gather per-unit results (mll, grad, mu, var, status) from all ranks into global order on
-    `dst`; returns the assembled dict on dst and None elsewhere."""
-    dist = _dist()
-    world = dist.get_world_size()
-    payload = {"index": list(index)}
-    for k in ("mll", "grad", "mu", "var", "status", "info"):
-        v = local.get(k)
-        payload[k] = None if v is None else np.asarray(v)
-    objs = [None] * world if dist.get_rank() == dst else None
-    dist.gather_object(payload, objs, dst=dst)
-    if dist.get_rank() != dst:
-        return None
-    out: dict = {}
-    for p in objs:
-        for k, v in p.items():
-            if k == "index" or v is None:
-                continue
-            if k not in out:
-                out[k] = np.zeros((n_total,) + v.shape[1:], dtype=v.dtype)
-            out[k][p["index"]] = v
-    return out
-
-
-def run_trials_sharded(trials: Sequence[dict], evaluate: Callable, dst: int = 0):
+def run_trials_sharded(n_trials: int, get_trial: Callable[[int], dict], evaluate: Callable, dst: int | None = 0):
     """Evaluate every (trial, output) unit, trials sharded over ranks; results gathered on dst.
 
-    trials[i] = dict(X (d,N), Y (G,N), theta (G,d+2), Xs (d,M) or None); all with equal G.
-    Returns dict of arrays shaped (n_trials, G, ...) on dst, None elsewhere.
-    """
+    get_trial(t) -> dict(X (d,N), Y (G,N), theta (G,d+2), Xs (d,M) or None) is called only for the
+    rank's own trials (inputs are made or loaded where they are evaluated); evaluate(local_trials)
+    -> dict of (n_local, G, ...) arrays (RankBatch / gpu_evaluator on the GPU).  Returns dict of
+    arrays shaped (n_trials, G, ...) on dst (every rank when dst is None), None elsewhere."""
     dist = _dist()
     rank, world = dist.get_rank(), dist.get_world_size()
-    mine = shard_trials(len(trials), rank, world)
-    G = trials[0]["Y"].shape[0]
-    local: dict = {}
-    index = []
-    for t in mine:
-        tr = trials[t]
-        r = evaluate(tr["X"], tr["Y"], tr["theta"], tr.get("Xs"))
-        for k, v in r.items():
-            if v is None:
-                continue
-            local.setdefault(k, []).append(np.asarray(v))
-        index.extend(range(t * G, (t + 1) * G))
-    local = {k: np.concatenate(v, axis=0) for k, v in local.items()}
-    out = gather_results(local, len(trials) * G, index, dst)
+    mine = shard_trials(n_trials, rank, world)
+    trials = [get_trial(t) for t in mine]
+    local = evaluate(trials) if trials else {}
+    local = {k: v for k, v in local.items() if np.ndim(v) >= 2}  # per-unit arrays only
+    # ranks without trials (n_trials < world) still take part in every gather: G and the result
+    # layout come from rank 0, which always holds trial 0
+    G, keys = _agree_keys((np.atleast_2d(trials[0]["Y"]).shape[0], describe(local)) if rank == 0 else None)
+    if not trials:
+        local = _empty_like_remote(keys, G)
+    flat = {k: np.asarray(v).reshape((-1,) + np.asarray(v).shape[2:]) for k, v in local.items()}
+    out = gather_results(flat, n_trials * G, lambda r: [t * G + g for t in shard_trials(n_trials, r, world)
+                                                         for g in range(G)], dst, keys=[k for k, _, _ in keys])
     if out is None:
         return None
-    return {k: v.reshape((len(trials), G) + v.shape[1:]) for k, v in out.items()}
+    return {k: v.reshape((n_trials, G) + v.shape[1:]) for k, v in out.items()}
+
+
+def _agree_keys(meta):
+    """Every rank learns rank 0's result layout (object broadcast of a few bytes of metadata; the
+    data itself travels as tensors)."""
+    dist = _dist()
+    obj = [meta]
+    dist.broadcast_object_list(obj, src=0)
+    return obj[0]
+
+
+def _empty_like_remote(keys, G):
+    return {k: np.zeros((0, G) + tuple(shape), dtype=dt) for k, shape, dt in keys}
+
+
+def describe(local: dict):
+    """(key, trailing shape after (n_local, G), dtype str) per result array."""
+    return [(k, tuple(np.asarray(v).shape[2:]), str(np.asarray(v).dtype)) for k, v in sorted(local.items())]
 
 
 def run_trial_split(trial: dict | None, evaluate: Callable, src: int = 0):
     """One trial whose G outputs are spread over the ranks: src broadcasts X/Y/theta/Xs, rank r
-    evaluates outputs k ≡ r (mod world), results are gathered on src."""
+    evaluates outputs k = r (mod world), results are gathered on src.  evaluate([trial]) as for
+    run_trials_sharded."""
     dist = _dist()
     rank, world = dist.get_rank(), dist.get_world_size()
     if rank == src:
         X, Y, th, Xs = broadcast_trial(trial["X"], trial["Y"], trial["theta"], trial.get("Xs"), src)
     else:
         X, Y, th, Xs = broadcast_trial(None, None, None, None, src)
-    ks = shard_outputs(Y.shape[0], rank, world)
-    local = evaluate(X, Y[ks], th[ks], Xs) if ks else {}
-    return gather_results(local, Y.shape[0], ks, src)
+    G = Y.shape[0]
+    ks = shard_outputs(G, rank, world)
+    local = evaluate([dict(X=X, Y=Y[ks], theta=th[ks], Xs=Xs)]) if ks else {}
+    local = {k: v for k, v in local.items() if np.ndim(v) >= 2}
+    keys = _agree_keys(describe(local) if rank == 0 else None)
+    flat = {k: np.asarray(v)[0] for k, v in local.items()} if ks else {k: np.zeros((0,) + tuple(s), dtype=dt)
+                                                                        for k, s, dt in keys}
+    return gather_results(flat, G, lambda r: shard_outputs(G, r, world), src, keys=[k for k, _, _ in keys])

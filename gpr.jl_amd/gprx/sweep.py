@@ -1,0 +1,223 @@
+"""The noise.jl sweep on MI355X: {P1, P2, CP, FB} x dataset sizes x trials, trial-sharded over the
+ranks of a torch.distributed group (examples/noise.jl:78-116 over examples/parallel/core.jl:27-89).
+
+The reference runs, per (experiment, N), `parallelsim(experiment, expand_config(ID, N, ...))`:
+`Threads.@threads for jobid in 1:nruns` (core.jl:28), each job one trial:
+
+    GP(X, y_k, MeanZero(), SEArd(theta0)) ; optimize!(gp, LBFGS(BackTracking(order=2)),
+    Options(time_limit=10.)) for every output k     (e.g. P2noise.jl:37-43, P2noise.jl(min):68-71)
+    predictdynamics / predictdynamicsmin for the 100 test samples, 20 steps   (:45-51 / :73-76)
+    kstep_mse = simulationerror(xtest_future_true, predictions)               (core.jl:75-76)
+
+Here one rank holds its trials' G outputs as ONE device batch (shard.RankBatch: B = local
+trials x G), optimises every GP at once with the device LBFGS (k_lbfgs; a fixed evaluation budget
+per GP replaces the machine-dependent 10 s cap, or a wall-clock limit for the whole call), and
+rolls out every test trajectory of every local trial in one launch (gprx_rollout_min).  Results
+are gathered as raw tensors (shard.gather_results) and written in the shape of the reference's
+final checkpoint (core.jl:79-82): {etype: {ID<N>: {nprocessed, kstep_mse[], projectionerror[]}}}.
+
+Variants (the MeanZero half of noise.jl's six; the MeanDynamics half runs CPU physics per
+training column, SURVEY.md section 2 rows 3/22, out of scope):
+    max      maximal coordinates, CState inputs (experiment_*_mz_max): optimise; one-step
+             predictions of the vw outputs at the test CStates (the rollout needs projectv! +
+             the rigid-body update: gprx.projection), error = mean squared one-step error
+    min      minimal coordinates (experiment_*_mz_min): optimise + 20-step device rollout, error =
+             simulationerror of the final CStates (position MSE)
+    min_sin  as min with (sin, cos) angle features (experiment_*_mz_min_sin)
+Data are the synthetic generator's (gprx.data; the .jls datasets are absent), seeded per
+(mechanism, trial) as 1000 * config_id + trial (data.trial_seed).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import time
+
+import numpy as np
+
+from . import data, shard
+from .rollout import NCOORD, final_cstate, rollout_min
+
+MECHS = ("P1", "P2", "CP", "FB")
+SIZES = (2, 4, 8, 16, 32, 64, 128, 256, 512)  # noise.jl:64
+VARIANTS = ("max", "min", "min_sin")
+ETYPE = {"max": "noisy", "min": "noisy", "min_sin": "noisysin"}  # parallelsim idmod (noise.jl:82-84)
+
+
+def _dist():
+    import torch.distributed as dist
+
+    return dist if dist.is_available() and dist.is_initialized() else None
+
+
+def local_trials(mech: str, N: int, variant: str, trial_ids, testsamples: int) -> list[dict]:
+    """The trials' GP inputs, built on the rank that owns them."""
+    out = []
+    for t in trial_ids:
+        seed = data.trial_seed(mech, t)
+        if variant == "max":
+            tr = data.make_trial(mech, N, testsamples, seed=seed)
+            th = data.theta0(mech, N, "MAX")
+            out.append(dict(X=tr["X"], Y=tr["Y"], Xs=tr["Xs"], theta=np.tile(th, (tr["Y"].shape[0], 1)), trial=t,
+                            seed=seed))
+        else:
+            usesin = variant == "min_sin"
+            tr = data.make_trial_min(mech, N, testsamples, seed=seed, usesin=usesin)
+            th = data.theta0_min(mech, N, usesin)
+            out.append(dict(X=tr["X"], Y=tr["Y"], Xs=None, start=tr["start"], theta=np.tile(th, (tr["Y"].shape[0], 1)),
+                            trial=t, seed=seed))
+    return out
+
+
+def run_group(mech: str, N: int, variant: str, trial_ids, ctx, testsamples: int = 100, simsteps: int = 20,
+              max_evals: int | None = 30, time_limit: float = float("nan"), keep: bool = False) -> dict:
+    """One (mechanism, N, variant) group for this rank's trials: device optimise of every GP,
+    then the variant's evaluation.  Returns per-trial arrays (n_local, ...) and timings."""
+    from .optim import LBFGS, Options
+
+    trials = local_trials(mech, N, variant, trial_ids, testsamples)
+    n = len(trials)
+    if n == 0:
+        return {}
+    t0 = time.perf_counter()
+    rb = shard.RankBatch(trials, ctx=ctx)
+    th0 = np.stack([t["theta"] for t in trials])
+    opt = rb.optimize(th0, LBFGS(), Options(max_evals=max_evals, time_limit=time_limit))
+    t_opt = time.perf_counter() - t0
+    G = rb.G
+    ok_gp = opt["status"] == 0  # (n, G)
+    err = np.full(n, math.inf)
+    t1 = time.perf_counter()
+    if variant == "max":
+        # one-step predictions of the vw outputs at the test CStates (the refit's mean-only
+        # prediction) against the next-step targets of those states
+        for i, tr in enumerate(trials):
+            nxt = _next_outputs(mech, tr["seed"], testsamples)
+            if np.all(ok_gp[i]):
+                err[i] = float(np.mean((opt["mu"][i] - nxt) ** 2))
+    else:
+        usesin = variant == "min_sin"
+        nc = NCOORD[mech]
+        good = [i for i in range(n) if np.all(ok_gp[i])]
+        if good:
+            groups = [[(rb.batch, rb.slot(i, g)) for g in range(nc)] for i in good]
+            start = np.concatenate([trials[i]["start"] for i in good])
+            tg = np.repeat(np.arange(len(good), dtype=np.int32), testsamples)
+            fin = rollout_min(mech, groups, start, simsteps, usesin=usesin, traj_group=tg, ctx=ctx)
+            for k, i in enumerate(good):
+                f = fin[k * testsamples:(k + 1) * testsamples]
+                pred = np.stack([final_cstate(mech, row[0::2]) for row in f])
+                truth = data.test_truth(mech, testsamples, trials[i]["seed"], simsteps)["X"].T
+                err[i] = data.position_mse(truth, pred)
+    t_eval = time.perf_counter() - t1
+    out = dict(kstep_mse=err, mll=opt["mll"], theta=opt["theta"], status=opt["status"], f_calls=opt["f_calls"],
+               rounds=opt["rounds"], t_opt=t_opt, t_eval=t_eval, slots=n * G)
+    if keep:
+        out.update(rb=rb, trials=trials)
+    else:
+        rb.close()
+    return out
+
+
+def _next_outputs(mech: str, seed: int, M: int) -> np.ndarray:
+    """Next-step vw outputs of the test states (the generator's own step of the clean draws, as
+    make_trial builds its training targets): (G, M)."""
+    rng_t = np.random.default_rng(seed + 500000)
+    m = data._sample_minimal(mech, M, rng_t)
+    Xn = data._cstates(mech, data._step(mech, m))
+    return np.stack([Xn[i - 1] for i in data.VW_INDICES[mech]])
+
+
+def run(mechs=MECHS, sizes=SIZES, variants=VARIANTS, n_trials: int = 100, testsamples: int = 100, simsteps: int = 20,
+        max_evals: int | None = 30, time_limit: float = float("nan"), ctx=None, log=None) -> dict:
+    """The sweep.  Every rank runs its trials of every group; rank 0 returns the gathered
+    checkpoint dict (other ranks None).  Without an initialised process group: one rank."""
+    from .batch import Context
+
+    dist = _dist()
+    rank, world = (dist.get_rank(), dist.get_world_size()) if dist else (0, 1)
+    if ctx is None:
+        import torch
+
+        ctx = Context(torch.cuda.current_device())
+    mine = shard.shard_trials(n_trials, rank, world)
+    results: dict = {}
+    timing: dict = {}
+    for mech in mechs:
+        for N in sizes:
+            for var in variants:
+                r = run_group(mech, N, var, mine, ctx, testsamples, simsteps, max_evals, time_limit)
+                local = {"kstep_mse": r.get("kstep_mse", np.zeros(0)),
+                         "ok": np.all(r["status"] == 0, axis=1).astype(np.float64) if r else np.zeros(0),
+                         "t": np.full(len(mine), r.get("t_opt", 0.0) + r.get("t_eval", 0.0))}
+                if dist:
+                    g = shard.gather_results({k: v.reshape(-1, 1) for k, v in local.items()}, n_trials,
+                                             lambda q: shard.shard_trials(n_trials, q, world), 0,
+                                             keys=("kstep_mse", "ok", "t"))
+                else:
+                    g = {k: v.reshape(-1, 1) for k, v in local.items()}
+                key = f"{mech}_{'MAX' if var == 'max' else 'MIN'}{N}"
+                if rank == 0:
+                    ks = [None if not math.isfinite(float(v)) else float(v) for v in g["kstep_mse"][:, 0]]
+                    et = ETYPE[var]
+                    results.setdefault(et, {})[key] = {"nprocessed": n_trials, "kstep_mse": ks,
+                                                       "projectionerror": [0.0] * n_trials,
+                                                       "variant": var, "ok": int(g["ok"][:, 0].sum())}
+                    timing[f"{key}/{var}"] = {"seconds_max_rank": float(np.max(g["t"][:, 0])) if n_trials else 0.0,
+                                              "gp_fits": n_trials * (len(data.VW_INDICES[mech]) if var == "max"
+                                                                     else NCOORD[mech])}
+                    if log:
+                        log(f"{key} {var}: ok {results[et][key]['ok']}/{n_trials}, "
+                            f"{timing[f'{key}/{var}']['seconds_max_rank']:.3f} s")
+    if rank != 0:
+        return None
+    return {"results": results, "timing": timing, "world": world, "n_trials": n_trials, "max_evals": max_evals,
+            "time_limit": time_limit, "testsamples": testsamples, "simsteps": simsteps}
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--mechs", default=",".join(MECHS))
+    ap.add_argument("--sizes", default=",".join(map(str, SIZES)))
+    ap.add_argument("--variants", default=",".join(VARIANTS))
+    ap.add_argument("--trials", type=int, default=100)
+    ap.add_argument("--testsamples", type=int, default=100)
+    ap.add_argument("--simsteps", type=int, default=20)
+    ap.add_argument("--max-evals", type=int, default=30, help="evaluation budget per GP (<0: none)")
+    ap.add_argument("--time-limit", type=float, default=float("nan"), help="seconds per group call (NaN: none)")
+    ap.add_argument("--out", default="gpurun_out/sweep_final_checkpoint.json")
+    a = ap.parse_args(argv)
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl" if torch.cuda.device_count() >= world else "gloo")
+    t0 = time.perf_counter()
+    res = run([m for m in a.mechs.split(",") if m], [int(s) for s in a.sizes.split(",") if s],
+              [v for v in a.variants.split(",") if v], a.trials, a.testsamples, a.simsteps,
+              None if a.max_evals < 0 else a.max_evals, a.time_limit,
+              log=lambda s: print(s, flush=True))
+    wall = time.perf_counter() - t0
+    if res is not None:
+        res["wall_seconds"] = wall
+        os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
+        with open(a.out, "w") as f:
+            json.dump(res, f)
+        fits = sum(v["gp_fits"] for v in res["timing"].values())
+        print(json.dumps({"sweep_wall_s": round(wall, 3), "groups": len(res["timing"]), "gp_optimisations": fits,
+                          "world": res["world"], "out": a.out}), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -47,6 +47,20 @@ for k, cs in pmc.items():
         e["l2_hit"] = avg["TCC_HIT_sum"] / max(1.0, avg["TCC_HIT_sum"] + avg["TCC_MISS_sum"])
     if "SQ_INSTS_VALU_MFMA_F64" in avg:
         e["mfma_f64_insts_per_launch"] = avg["SQ_INSTS_VALU_MFMA_F64"]
+    if "SQ_INSTS_VALU" in avg:
+        # VALU issue floor: every wave64 fp64 VALU instruction occupies its SIMD-32 for >= 4
+        # cycles (78.6 TF/s fp64 vector = 16 FMA lanes/clk/SIMD); 1024 SIMDs; clock = GRBM_GUI_ACTIVE
+        # (summed over the 8 XCDs) / 8 / duration.  valu_floor_frac = floor / duration: near 1
+        # means VALU-issue-bound (transcendentals cost more, so this is a lower bound)
+        e["valu_insts_per_launch"] = avg["SQ_INSTS_VALU"]
+        if "SQ_ACTIVE_INST_VALU" in avg:
+            e["active_inst_valu_per_launch"] = avg["SQ_ACTIVE_INST_VALU"]
+        if "GRBM_GUI_ACTIVE" in avg and e.get("avg_ms"):
+            dur = e["avg_ms"] * 1e-3
+            clk = avg["GRBM_GUI_ACTIVE"] / 8.0 / dur
+            e["clock_ghz_est"] = clk / 1e9
+            e["valu_floor_ms"] = avg["SQ_INSTS_VALU"] * 4.0 / 1024.0 / clk * 1e3
+            e["valu_floor_frac"] = e["valu_floor_ms"] / e["avg_ms"]
 
 bench = None
 try:

@@ -1,0 +1,165 @@
+"""The noise.jl sweep (BASELINE config 5) through the product sharding path on the GPU: a reduced
+sweep (4 mechanisms x 3 sizes x 8 trials, the three MeanZero variants) through
+gprx.sweep.run_group (one shard.RankBatch per group: B = trials x outputs, device LBFGS, device
+rollouts) checked against the oracle, and gprx.sweep.run under a world-size-1 gloo group (the
+gather path).  Plus the FB hyperparameter.jl-shaped optimise loop at the BASELINE size N=4096.
+
+Oracle checks: the LML at every checked minimiser (oracle fit at the device's theta*), the k-step
+rollout final states (oracle rollout with the oracle's alpha at theta*), and the error metric
+recomputed on the host.  Tolerances as tests/test_gpu.py (LML) and tests/test_rollout.py
+(rollouts: 10x the oracle's distance-mode spread)."""
+import math
+import os
+import socket
+
+import numpy as np
+import pytest
+import scipy.linalg as sla
+
+pytestmark = pytest.mark.gpu
+
+from oracle import gp_oracle as O  # noqa: E402
+
+MECHS = ("P1", "P2", "CP", "FB")
+SIZES = (8, 64, 256)
+TRIALS = 8
+TESTS = 16
+STEPS = 20
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    import gprx
+
+    c = gprx.Context(0)
+    yield c
+    c.close()
+
+
+def _mll_ok(got, X, y, th, mode):
+    f = O.fit(X, y, th, None, mode)
+    f2 = O.fit(X, y, th, None, 1 - mode)
+    tol = max(1e-9 * max(1.0, abs(f["mll"])), 10 * abs(f["mll"] - f2["mll"]), 10 * f["mll_sens"])
+    return abs(got - f["mll"]) <= tol, (got, f["mll"], tol)
+
+
+@pytest.mark.parametrize("mech", MECHS)
+def test_reduced_sweep_against_oracle(ctx, mech):
+    from gprx import data, sweep
+    from gprx.rollout import NCOORD, final_cstate
+
+    mode = ctx.dist_mode
+    for N in SIZES:
+        for var in sweep.VARIANTS:
+            r = sweep.run_group(mech, N, var, range(TRIALS), ctx, testsamples=TESTS, simsteps=STEPS, max_evals=20,
+                                keep=True)
+            rb, trials = r["rb"], r["trials"]
+            G = rb.G
+            assert r["kstep_mse"].shape == (TRIALS,) and r["status"].shape == (TRIALS, G)
+            assert np.all(r["f_calls"] <= 21)
+            for t in (0, TRIALS - 1):  # the LML at the device minimisers against the oracle
+                for g in range(G):
+                    if r["status"][t, g] != 0:
+                        continue
+                    ok, info = _mll_ok(r["mll"][t, g], trials[t]["X"], np.atleast_2d(trials[t]["Y"])[g],
+                                       r["theta"][t, g], mode)
+                    assert ok, (mech, N, var, t, g, info)
+            if var == "max":
+                assert np.sum(np.isfinite(r["kstep_mse"])) >= TRIALS // 2, (mech, N, r["status"])
+                continue
+            usesin = var == "min_sin"
+            nc = NCOORD[mech]
+            for t in (0, TRIALS - 1):
+                if not np.all(r["status"][t] == 0):
+                    continue
+                tr = trials[t]
+                # three legitimate formulations: the oracle in this distance mode (reference), in the
+                # other mode, and with alpha by an LU solve instead of the Cholesky solve -- after
+                # optimisation K can be ill-conditioned, and the 20-step rollout carries alpha's
+                # rounding (cond(K) eps) forward; the tolerance is 10x the largest spread
+                gps, gps2, gps3 = [], [], []
+                for g in range(nc):
+                    th = r["theta"][t, g]
+                    gps.append((tr["X"], th, O.fit(tr["X"], tr["Y"][g], th, None, mode)["alpha"]))
+                    gps2.append((tr["X"], th, O.fit(tr["X"], tr["Y"][g], th, None, 1 - mode)["alpha"]))
+                    K = O.gram(tr["X"], th, mode)[0]
+                    gps3.append((tr["X"], th, sla.solve(K, tr["Y"][g], assume_a="gen")))
+                truth = data.test_truth(mech, TESTS, tr["seed"], STEPS)["X"].T
+
+                def kerr(gl, md):
+                    fin = O.rollout_min(mech, gl, tr["start"], STEPS, usesin, mode=md)
+                    return data.position_mse(truth, np.stack([final_cstate(mech, row[0::2]) for row in fin]))
+
+                err_ref, err_alt, err_lu = kerr(gps, mode), kerr(gps2, 1 - mode), kerr(gps3, mode)
+                spread = max(abs(err_ref - err_alt), abs(err_ref - err_lu))
+                tol = max(1e-9 * max(1.0, abs(err_ref)), 10 * spread)
+                assert abs(r["kstep_mse"][t] - err_ref) <= tol, (mech, N, var, t, r["kstep_mse"][t], err_ref, tol)
+            rb.close()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_sweep_run_gathers_through_a_process_group(ctx):
+    """gprx.sweep.run under an initialised (gloo, world 1) group: the gathered checkpoint equals
+    the per-group results, in the reference's final-checkpoint shape (core.jl:79-82)."""
+    import torch.distributed as dist
+
+    from gprx import sweep
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        res = sweep.run(("P2", "CP"), (16,), ("min", "max"), n_trials=4, testsamples=TESTS, simsteps=STEPS,
+                        max_evals=10, ctx=ctx)
+    finally:
+        dist.destroy_process_group()
+    assert set(res["results"]["noisy"]) == {"P2_MIN16", "P2_MAX16", "CP_MIN16", "CP_MAX16"}
+    e = res["results"]["noisy"]["P2_MIN16"]
+    assert e["nprocessed"] == 4 and len(e["kstep_mse"]) == 4
+    r = sweep.run_group("P2", 16, "min", range(4), ctx, TESTS, STEPS, 10)
+    np.testing.assert_array_equal([math.inf if v is None else v for v in e["kstep_mse"]], r["kstep_mse"])
+
+
+def test_fb_hyperparameter_optimise_n4096(ctx):
+    """examples/hyperparameter.jl:50-60 -> FBparam.jl shape at the BASELINE size: FB, N=4096,
+    d=52, the 12 output GPs of one trial, random-restart start theta (CPparam.jl:28-31: theta =
+    [100, 50 ./ std(X)] jittered), MeanZero, device LBFGS + BackTracking(order=2) with a
+    30-evaluation budget.  The LML at the minimisers against the oracle; the optimiser improves
+    every slot it does not fail on."""
+    import gprx
+    from gprx import data
+    from gprx.optim import LBFGS, Options
+
+    tr = data.make_trial("FB", 4096, 0, seed=data.trial_seed("FB", 1))
+    X, Y = tr["X"], tr["Y"]
+    G = Y.shape[0]
+    rng = np.random.default_rng(4096)
+    stdx = X.std(axis=1, ddof=1)
+    stdx[stdx == 0] = 1000.0
+    p0 = np.concatenate([[100.0], 50.0 / stdx])
+    th0 = []
+    for _ in range(G):
+        p = p0 + (5 * rng.random(p0.shape[0]) - 0.999) * p0
+        th0.append(data.theta_from_params(p))
+    th0 = np.stack(th0)
+    b = gprx.GPBatch(G, 52, 4096, 0, ctx=ctx)
+    b.set_train(X, Y)
+    start = b.run(th0, grad=False)
+    res, rounds = b.optimize(th0, LBFGS(), Options(max_evals=30), refit=True)
+    assert rounds <= 31
+    thmin = np.stack([x.minimizer for x in res])
+    r = b.run(thmin, grad=False)
+    for s in range(G):
+        assert res[s].f_calls + res[s].g_calls <= 31
+        if start["status"][s] == 0:
+            assert r["mll"][s] >= start["mll"][s]
+    for s in (0, 5, 11):
+        ok, info = _mll_ok(r["mll"][s], X, Y[s], thmin[s], ctx.dist_mode)
+        assert ok, (s, info)
+    b.close()
