@@ -939,6 +939,220 @@ int gprx_rollout_min(gprx_ctx* c, int mech, int usesin, double dt, int steps, in
   return GPRX_OK;
 }
 
+// ---- maximal-coordinate physics -----------------------------------------------------------------
+// The experiment mechanisms' joints (examples/utils/data/simulations.jl; oracle/projection_oracle.py
+// mechanism()): sub-joints in the order of the equality constraints and their rows.
+static bool build_mech(int mech, gprx::MechDev& M) {
+  M = gprx::MechDev{};
+  struct Sj {
+    int kind, rows, a, b;
+    double pa[3], pb[3], axis[3];
+  };
+  std::vector<Sj> js;
+  const double O[3] = {0, 0, 0}, EX[3] = {1, 0, 0}, EY[3] = {0, 1, 0};
+  auto add = [&](int kind, int rows, int a, int b, const double* pa, const double* pb, const double* ax) {
+    Sj j{kind, rows, a, b, {pa[0], pa[1], pa[2]}, {pb[0], pb[1], pb[2]}, {ax[0], ax[1], ax[2]}};
+    js.push_back(j);
+  };
+  auto rev = [&](int a, int b, const double* ax, const double* pa, const double* pb) {
+    add(0, 3, a, b, pa, pb, ax);  // Translational3
+    add(1, 2, a, b, pa, pb, ax);  // Rotational2 (free about the axis)
+  };
+  const double h1[3] = {0, 0, 0.5}, h1m[3] = {0, 0, -0.5}, hcp[3] = {0, 0, 0.25};
+  switch (mech) {
+    case GPRX_MECH_P1: M.nb = 1; rev(0, 1, EX, O, h1); break;
+    case GPRX_MECH_P2: M.nb = 2; rev(0, 1, EX, O, h1); rev(1, 2, EX, h1m, h1); break;
+    case GPRX_MECH_CP:
+      M.nb = 2;
+      add(0, 2, 0, 1, O, O, EY);  // Prismatic: Translational2 (free along y) + Rotational3
+      add(1, 3, 0, 1, O, O, EY);
+      rev(1, 2, EX, O, hcp);
+      break;
+    case GPRX_MECH_FB:
+      M.nb = 4;
+      rev(0, 1, EX, O, h1);
+      rev(1, 2, EX, h1m, h1);
+      add(0, 2, 1, 3, h1, h1, EX);  // Cylindrical: Translational2 + Rotational2
+      add(1, 2, 1, 3, h1, h1, EX);
+      rev(3, 4, EX, h1m, h1);
+      rev(2, 4, EX, h1m, h1m);
+      break;
+    default: return false;
+  }
+  int row = 0;
+  M.nsub = (int)js.size();
+  for (int k = 0; k < M.nsub; ++k) {
+    gprx::SubJoint& S = M.sub[k];
+    const Sj& j = js[k];
+    S.kind = j.kind;
+    S.a = j.a;
+    S.b = j.b;
+    S.rows = j.rows;
+    S.row0 = row;
+    row += j.rows;
+    for (int i = 0; i < 3; ++i) {
+      S.pa[i] = j.pa[i];
+      S.pb[i] = j.pb[i];
+    }
+    if (j.rows == 3) {
+      for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) S.C[r][c] = r == c ? 1.0 : 0.0;
+    } else {  // two orthonormal rows normal to the axis (oracle normal_rows)
+      const double* a = j.axis;
+      const double na = std::sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
+      const double u[3] = {a[0] / na, a[1] / na, a[2] / na};
+      const double t[3] = {std::fabs(u[2]) < 0.9 ? 0.0 : 1.0, 0.0, std::fabs(u[2]) < 0.9 ? 1.0 : 0.0};
+      double v1[3] = {u[1] * t[2] - u[2] * t[1], u[2] * t[0] - u[0] * t[2], u[0] * t[1] - u[1] * t[0]};
+      const double n1 = std::sqrt(v1[0] * v1[0] + v1[1] * v1[1] + v1[2] * v1[2]);
+      for (double& x : v1) x /= n1;
+      const double v2[3] = {u[1] * v1[2] - u[2] * v1[1], u[2] * v1[0] - u[0] * v1[2], u[0] * v1[1] - u[1] * v1[0]};
+      for (int c = 0; c < 3; ++c) {
+        S.C[0][c] = v1[c];
+        S.C[1][c] = v2[c];
+        S.C[2][c] = 0.0;
+      }
+    }
+  }
+  M.nd = row;
+  return 6 * M.nb + M.nd <= gprx::PJ_MAXN;
+}
+
+// device scratch of a context for the physics calls: [args | in | out], grown on demand
+static int ctx_scratch(gprx_ctx* c, size_t need, char** base) {
+  if (need > c->rcap) {
+    if (c->rbuf) HIPCHK(c, hipFree(c->rbuf));
+    c->rbuf = nullptr;
+    c->rcap = 0;
+    HIPCHK(c, hipMalloc(&c->rbuf, need));
+    c->rcap = need;
+  }
+  *base = (char*)c->rbuf;
+  return GPRX_OK;
+}
+static size_t al16(size_t x) { return (x + 15) / 16 * 16; }
+
+int gprx_projectv(gprx_ctx* c, int mech, double dt, int T, const double* cstates, const double* vw_pred,
+                  double regularizer, int newton_iter, double eps, double* vw_out, int* iterations, int* status) {
+  if (!c) return GPRX_INVALID_ARGUMENT;
+  gprx::MechDev M;
+  if (!build_mech(mech, M) || T < 0 || newton_iter < 0 || !(dt > 0.0) || !std::isfinite(regularizer) || !(eps >= 0.0))
+    return set_err(c, GPRX_INVALID_ARGUMENT, "gprx_projectv: bad mechanism / T / newton_iter / dt / regularizer / eps");
+  if (T == 0) return GPRX_OK;
+  if (!cstates || !vw_pred || !vw_out) return set_err(c, GPRX_INVALID_ARGUMENT, "gprx_projectv: null argument");
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess) return GPRX_DEVICE_ERROR;
+  const int nb = M.nb;
+  const size_t o_cs = 0, o_vw = al16(o_cs + (size_t)T * 13 * nb * 8), o_out = al16(o_vw + (size_t)T * 6 * nb * 8),
+               o_it = al16(o_out + (size_t)T * 6 * nb * 8), o_st = al16(o_it + (size_t)T * 4), need = al16(o_st + (size_t)T * 4);
+  char* base;
+  int rc = ctx_scratch(c, need, &base);
+  if (rc) return rc;
+  HIPCHK(c, hipMemcpyAsync(base + o_cs, cstates, (size_t)T * 13 * nb * 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(base + o_vw, vw_pred, (size_t)T * 6 * nb * 8, hipMemcpyHostToDevice, c->stream));
+  gprx::ProjArgs a{};
+  a.mech = M;
+  a.dt = dt;
+  a.reg = regularizer;
+  a.eps = eps;
+  a.iters = newton_iter;
+  a.T = T;
+  a.cs = (const double*)(base + o_cs);
+  a.vw = (const double*)(base + o_vw);
+  a.out = (double*)(base + o_out);
+  a.iters_out = (int*)(base + o_it);
+  a.status = (int*)(base + o_st);
+  timed(c, c->stream, "projectv", 0.0, (double)T * 8.0 * (13 + 12) * nb, [&] { gprx::launch_project(a, c->stream); });
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(vw_out, base + o_out, (size_t)T * 6 * nb * 8, hipMemcpyDeviceToHost, c->stream));
+  std::vector<int> it(T), st(T);
+  HIPCHK(c, hipMemcpyAsync(it.data(), base + o_it, (size_t)T * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(st.data(), base + o_st, (size_t)T * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  collect(c);
+  if (iterations) memcpy(iterations, it.data(), (size_t)T * 4);
+  if (status) memcpy(status, st.data(), (size_t)T * 4);
+  return GPRX_OK;
+}
+
+int gprx_rollout_max(gprx_ctx* c, int mech, double dt, int steps, double regularizer, int ngroups,
+                     gprx_batch* const* batches, const int* slots, int G, const int* vw_idx1, int T,
+                     const int* traj_group, const double* start, double* final_state, double* proj_err, int* status) {
+  if (!c) return GPRX_INVALID_ARGUMENT;
+  gprx::MechDev M;
+  if (!build_mech(mech, M) || steps < 0 || ngroups < 1 || T < 0 || G < 1 || G > gprx::PJ_MAXG || !(dt > 0.0) ||
+      !std::isfinite(regularizer))
+    return set_err(c, GPRX_INVALID_ARGUMENT, "gprx_rollout_max: bad mechanism / steps / groups / G / dt / regularizer");
+  if (T == 0) return GPRX_OK;
+  if (!batches || !slots || !vw_idx1 || !traj_group || !start || !final_state)
+    return set_err(c, GPRX_INVALID_ARGUMENT, "gprx_rollout_max: null argument");
+  const int d = 13 * M.nb;
+  gprx::RolloutMaxArgs a{};
+  for (int g = 0; g < G; ++g) {
+    const int k = (vw_idx1[g] - 1) % 13;
+    if (vw_idx1[g] < 1 || vw_idx1[g] > d || k < 7)
+      return set_err(c, GPRX_INVALID_ARGUMENT, "gprx_rollout_max: vw index " + std::to_string(vw_idx1[g]) +
+                                                   " is not a velocity / angular-velocity slot of the CState");
+    a.vw[g] = vw_idx1[g] - 1;
+  }
+  std::lock_guard<std::mutex> lk(c->mu);
+  std::vector<gprx::RolloutGP> gps((size_t)ngroups * G);
+  for (size_t k = 0; k < gps.size(); ++k) {
+    gprx_batch* b = batches[k];
+    const int s = slots[k];
+    if (!b || b->ctx != c || s < 0 || s >= b->db.B)
+      return set_err(c, GPRX_INVALID_ARGUMENT, "gprx_rollout_max: GP " + std::to_string(k) + " is not a slot of a batch of this context");
+    if (b->db.d != d)
+      return set_err(c, GPRX_INVALID_ARGUMENT, "gprx_rollout_max: input dimension " + std::to_string(b->db.d) + " != 13 nbodies");
+    if (!b->factored) return set_err(c, GPRX_NOT_READY, "gprx_rollout_max: batch not factorised (run it first)");
+    if (b->h_status[s] != 0) return set_err(c, b->h_status[s], "gprx_rollout_max: slot " + std::to_string(s) + " failed its last evaluation");
+    const DevBatch& db = b->db;
+    gps[k] = gprx::RolloutGP{db.X + (size_t)s * db.Npad * db.d, db.alpha + (size_t)s * db.Npad, db.params + (size_t)s * db.pst, db.N, 0};
+  }
+  for (int t = 0; t < T; ++t)
+    if (traj_group[t] < 0 || traj_group[t] >= ngroups) return set_err(c, GPRX_INVALID_ARGUMENT, "gprx_rollout_max: trajectory group out of range");
+  if (hipSetDevice(c->device) != hipSuccess) return GPRX_DEVICE_ERROR;
+  const size_t o_grp = al16(gps.size() * sizeof(gprx::RolloutGP)), o_st = al16(o_grp + (size_t)T * 4),
+               o_out = al16(o_st + (size_t)T * d * 8), o_pe = al16(o_out + (size_t)T * d * 8),
+               o_ss = al16(o_pe + (size_t)T * 8), need = al16(o_ss + (size_t)T * 4);
+  char* base;
+  int rc = ctx_scratch(c, need, &base);
+  if (rc) return rc;
+  HIPCHK(c, hipMemcpyAsync(base, gps.data(), gps.size() * sizeof(gprx::RolloutGP), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(base + o_grp, traj_group, (size_t)T * 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(base + o_st, start, (size_t)T * d * 8, hipMemcpyHostToDevice, c->stream));
+  a.mech = M;
+  a.dt = dt;
+  a.reg = regularizer;
+  a.eps = 1e-10;  // projectv! defaults (implicitProjection.jl:80)
+  a.iters = 100;
+  a.steps = steps;
+  a.T = T;
+  a.G = G;
+  a.d = d;
+  a.gps = (const gprx::RolloutGP*)base;
+  a.group = (const int*)(base + o_grp);
+  a.start = (const double*)(base + o_st);
+  a.out = (double*)(base + o_out);
+  a.perr = (double*)(base + o_pe);
+  a.status = (int*)(base + o_ss);
+  double np = 0.0;
+  for (int t = 0; t < T; ++t)
+    for (int g = 0; g < G; ++g) np += gps[(size_t)traj_group[t] * G + g].N;
+  timed(c, c->stream, "rollout_max", np * steps * (3.0 * d + 24.0), np * steps * (d + 1) * 8.0,
+        [&] { gprx::launch_rollout_max(a, c->dist_mode, c->stream); });
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(final_state, base + o_out, (size_t)T * d * 8, hipMemcpyDeviceToHost, c->stream));
+  std::vector<double> pe(T);
+  std::vector<int> ss(T);
+  HIPCHK(c, hipMemcpyAsync(pe.data(), base + o_pe, (size_t)T * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(ss.data(), base + o_ss, (size_t)T * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  collect(c);
+  if (proj_err) memcpy(proj_err, pe.data(), (size_t)T * 8);
+  if (status) memcpy(status, ss.data(), (size_t)T * 4);
+  return GPRX_OK;
+}
+
 gprx_batch* gprx_gp_batch(gprx_gp* gp) { return gp ? gp->batch : nullptr; }
 
 // ---- host CState helpers -----------------------------------------------------------------------

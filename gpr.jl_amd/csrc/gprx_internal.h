@@ -111,6 +111,50 @@ struct RolloutArgs {
 };
 constexpr int ROLLOUT_DMAX = 6;
 
+// Maximal-coordinate physics of the rollout (gprx_projection.hip): the joint constraints of a
+// mechanism as sub-joints (Revolute = T3 + R2, Prismatic = T2 + R3, Cylindrical = T2 + R2), rows of
+// each written in the order of the reference's equality constraints.
+constexpr int PJ_MAXB = 4;    // bodies (FB)
+constexpr int PJ_MAXSUB = 12; // sub-joints
+constexpr int PJ_MAXN = 56;   // 6 nb + constraint rows (FB: 24 + 24 = 48)
+constexpr int PJ_MAXG = 16;   // GP outputs of one rollout group
+struct SubJoint {
+  int kind;       // 0 translational, 1 rotational
+  int a, b;       // parent (0 = origin) and child body, 1-based
+  int rows, row0; // constraint rows (2 or 3) and the first row among all constraint rows
+  double pa[3], pb[3];
+  double C[3][3]; // rows of the constraint matrix (I3, or the 2 rows normal to the axis)
+};
+struct MechDev {
+  int nb, nd, nsub;  // bodies, constraint rows, sub-joints
+  SubJoint sub[PJ_MAXSUB];
+};
+struct ProjArgs {
+  MechDev mech;
+  double dt, reg, eps;
+  int iters;          // newtonIter
+  int T;              // trajectories
+  const double* cs;   // T x 13 nb CStates (the mechanism state: xc, qc, vc, wc per body)
+  const double* vw;   // T x 6 nb predicted (v, w) per body (projectv!'s vu, wu)
+  double* out;        // T x 6 nb projected (v, w)
+  int* iters_out;     // T Newton iterations
+  int* status;        // T: 0 ok, 1 singular KKT matrix (Julia's F \ f throws)
+};
+struct RolloutMaxArgs {
+  MechDev mech;
+  double dt, reg, eps;
+  int iters, steps, T, G, d;
+  int vw[PJ_MAXG];      // 0-based CState position of output g (getvw)
+  const RolloutGP* gps; // ngroups x G
+  const int* group;     // T
+  const double* start;  // T x d
+  double* out;          // T x d final CStates
+  double* perr;         // T mean projection error per step
+  int* status;          // T
+};
+void launch_project(const ProjArgs& a, hipStream_t s);
+void launch_rollout_max(const RolloutMaxArgs& a, int dist_mode, hipStream_t s);
+
 // hyper-parameters -> kernel parameters for one slot, exactly as SEArd / GPE derive them:
 //   il2 = exp(-2 log ell), sf2 = exp(2 log sf), noise = exp(2 logNoise) + eps();
 // a non-finite theta is an ArgumentError (status GPRX_INVALID_ARGUMENT = 2, parameters 1).

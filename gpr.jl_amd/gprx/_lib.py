@@ -80,6 +80,10 @@ SIGNATURES = {
     "gprx_gp_batch": (_vp, [_vp]),
     "gprx_rollout_min": (C.c_int, [_vp, C.c_int, C.c_int, C.c_double, C.c_int, C.c_int, C.POINTER(_vp), _ip, C.c_int,
                                    _ip, _dp, _dp]),
+    "gprx_projectv": (C.c_int, [_vp, C.c_int, C.c_double, C.c_int, _dp, _dp, C.c_double, C.c_int, C.c_double, _dp, _ip,
+                                _ip]),
+    "gprx_rollout_max": (C.c_int, [_vp, C.c_int, C.c_double, C.c_int, C.c_double, C.c_int, C.POINTER(_vp), _ip, C.c_int,
+                                   _ip, C.c_int, _ip, _dp, _dp, _dp, _ip]),
     "gprx_cstate_pack": (C.c_int, [C.c_int, _dp, _dp, _dp, _dp, _dp]),
     "gprx_select_outputs": (C.c_int, [_dp, C.c_int, C.c_int, _ip, C.c_int, _dp]),
 }

@@ -18,9 +18,9 @@ final checkpoint (core.jl:79-82): {etype: {ID<N>: {nprocessed, kstep_mse[], proj
 
 Variants (the MeanZero half of noise.jl's six; the MeanDynamics half runs CPU physics per
 training column, SURVEY.md section 2 rows 3/22, out of scope):
-    max      maximal coordinates, CState inputs (experiment_*_mz_max): optimise; one-step
-             predictions of the vw outputs at the test CStates (the rollout needs projectv! +
-             the rigid-body update: gprx.projection), error = mean squared one-step error
+    max      maximal coordinates, CState inputs (experiment_*_mz_max): optimise + 20-step device
+             predictdynamics (GP means, projectv!, updatestate!: gprx.projection), error =
+             simulationerror of the final CStates, projectionerror = the mean projection error
     min      minimal coordinates (experiment_*_mz_min): optimise + 20-step device rollout, error =
              simulationerror of the final CStates (position MSE)
     min_sin  as min with (sin, cos) angle features (experiment_*_mz_min_sin)
@@ -89,14 +89,25 @@ def run_group(mech: str, N: int, variant: str, trial_ids, ctx, testsamples: int 
     G = rb.G
     ok_gp = opt["status"] == 0  # (n, G)
     err = np.full(n, math.inf)
+    perr = np.zeros(n)
     t1 = time.perf_counter()
     if variant == "max":
-        # one-step predictions of the vw outputs at the test CStates (the refit's mean-only
-        # prediction) against the next-step targets of those states
-        for i, tr in enumerate(trials):
-            nxt = _next_outputs(mech, tr["seed"], testsamples)
-            if np.all(ok_gp[i]):
-                err[i] = float(np.mean((opt["mu"][i] - nxt) ** 2))
+        # predictdynamics for every test CState of every good trial in one launch
+        from .projection import predictdynamics
+
+        good = [i for i in range(n) if np.all(ok_gp[i])]
+        if good:
+            groups = [[(rb.batch, rb.slot(i, g)) for g in range(G)] for i in good]
+            start = np.concatenate([trials[i]["Xs"].T for i in good])
+            tg = np.repeat(np.arange(len(good), dtype=np.int32), testsamples)
+            fin, pe, st = predictdynamics(mech, groups, start, simsteps, data.VW_INDICES[mech], traj_group=tg, ctx=ctx)
+            for k, i in enumerate(good):
+                sl = slice(k * testsamples, (k + 1) * testsamples)
+                if np.any(st[sl] != 0):  # a singular projection throws in the reference: trial dropped
+                    continue
+                truth = data.test_truth(mech, testsamples, trials[i]["seed"], simsteps)["X"].T
+                err[i] = data.position_mse(truth, fin[sl])
+                perr[i] = float(np.mean(pe[sl]))  # projectionerror / length(xtest_old) (P2noise.jl:51)
     else:
         usesin = variant == "min_sin"
         nc = NCOORD[mech]
@@ -112,22 +123,14 @@ def run_group(mech: str, N: int, variant: str, trial_ids, ctx, testsamples: int 
                 truth = data.test_truth(mech, testsamples, trials[i]["seed"], simsteps)["X"].T
                 err[i] = data.position_mse(truth, pred)
     t_eval = time.perf_counter() - t1
-    out = dict(kstep_mse=err, mll=opt["mll"], theta=opt["theta"], status=opt["status"], f_calls=opt["f_calls"],
+    out = dict(kstep_mse=err, projectionerror=perr, mll=opt["mll"], theta=opt["theta"], status=opt["status"],
+               f_calls=opt["f_calls"],
                rounds=opt["rounds"], t_opt=t_opt, t_eval=t_eval, slots=n * G)
     if keep:
         out.update(rb=rb, trials=trials)
     else:
         rb.close()
     return out
-
-
-def _next_outputs(mech: str, seed: int, M: int) -> np.ndarray:
-    """Next-step vw outputs of the test states (the generator's own step of the clean draws, as
-    make_trial builds its training targets): (G, M)."""
-    rng_t = np.random.default_rng(seed + 500000)
-    m = data._sample_minimal(mech, M, rng_t)
-    Xn = data._cstates(mech, data._step(mech, m))
-    return np.stack([Xn[i - 1] for i in data.VW_INDICES[mech]])
 
 
 def run(mechs=MECHS, sizes=SIZES, variants=VARIANTS, n_trials: int = 100, testsamples: int = 100, simsteps: int = 20,
@@ -149,13 +152,13 @@ def run(mechs=MECHS, sizes=SIZES, variants=VARIANTS, n_trials: int = 100, testsa
         for N in sizes:
             for var in variants:
                 r = run_group(mech, N, var, mine, ctx, testsamples, simsteps, max_evals, time_limit)
-                local = {"kstep_mse": r.get("kstep_mse", np.zeros(0)),
+                local = {"kstep_mse": r.get("kstep_mse", np.zeros(0)), "perr": r.get("projectionerror", np.zeros(0)),
                          "ok": np.all(r["status"] == 0, axis=1).astype(np.float64) if r else np.zeros(0),
                          "t": np.full(len(mine), r.get("t_opt", 0.0) + r.get("t_eval", 0.0))}
                 if dist:
                     g = shard.gather_results({k: v.reshape(-1, 1) for k, v in local.items()}, n_trials,
                                              lambda q: shard.shard_trials(n_trials, q, world), 0,
-                                             keys=("kstep_mse", "ok", "t"))
+                                             keys=("kstep_mse", "perr", "ok", "t"))
                 else:
                     g = {k: v.reshape(-1, 1) for k, v in local.items()}
                 key = f"{mech}_{'MAX' if var == 'max' else 'MIN'}{N}"
@@ -163,7 +166,7 @@ def run(mechs=MECHS, sizes=SIZES, variants=VARIANTS, n_trials: int = 100, testsa
                     ks = [None if not math.isfinite(float(v)) else float(v) for v in g["kstep_mse"][:, 0]]
                     et = ETYPE[var]
                     results.setdefault(et, {})[key] = {"nprocessed": n_trials, "kstep_mse": ks,
-                                                       "projectionerror": [0.0] * n_trials,
+                                                       "projectionerror": [float(v) for v in g["perr"][:, 0]],
                                                        "variant": var, "ok": int(g["ok"][:, 0].sum())}
                     timing[f"{key}/{var}"] = {"seconds_max_rank": float(np.max(g["t"][:, 0])) if n_trials else 0.0,
                                               "gp_fits": n_trials * (len(data.VW_INDICES[mech]) if var == "max"

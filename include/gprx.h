@@ -202,6 +202,30 @@ int gprx_rollout_min(gprx_ctx* ctx, int mech, int usesin, double dt, int steps, 
                      gprx_batch* const* batches, const int* slots, int T, const int* traj_group,
                      const double* start, double* final_state);
 
+/* ---- maximal-coordinate physics: projectv! and predictdynamics ----------------------------- */
+/* projectv!(vu, wu, mechanism; newtonIter, eps, regularizer)  src/projections/implicitProjection.jl:80-107
+ * for T independent mechanism states in one launch: state t is the mechanism's CState
+ * cstates[t*13nb ...] (setstates!: positions, quaternions, velocities; the discrete pose follows as
+ * x2 = x + v dt, q2 = q * wbar(w) dt/2), the prediction vw_pred[t*6nb ...] = (v_1, w_1, ..., v_nb,
+ * w_nb).  Outputs vw_out (the projected twists; NaN for a failed state), iterations[t], status[t]
+ * (0 ok, 1 singular KKT matrix: Julia's F \ f throws SingularException).  mech: GPRX_MECH_*, the
+ * experiment mechanisms of examples/utils/data/simulations.jl (P1 pendulum, P2 double pendulum,
+ * CP cart-pole, FB four-bar).  dt: mechanism.dt (0.01 in the experiments).                       */
+int gprx_projectv(gprx_ctx* ctx, int mech, double dt, int T, const double* cstates, const double* vw_pred,
+                  double regularizer, int newton_iter, double eps, double* vw_out, int* iterations, int* status);
+/* predictdynamics(mechanism, gps, startobservation, steps, getvw; regularizer)
+ * examples/utils/predictdynamics.jl:7-22 for T trajectories in one launch: per step the G GPs'
+ * mean predictions at the current CState (predict_y(gp, obs)[1][1], MeanZero), getvw (output g
+ * placed at 1-based CState position vw_idx1[g], a velocity or angular-velocity slot), projectv!
+ * and updatestate!; one closing updatestate!.  GPs as for gprx_rollout_min: (batches[k],
+ * slots[k]) for k = group*G + g, factorised, input dimension 13 nb.  Outputs final_state[t*13nb]
+ * (the predicted CState), proj_err[t] (mean projection error per step), status[t] (0 ok, 1
+ * singular projection).                                                                          */
+int gprx_rollout_max(gprx_ctx* ctx, int mech, double dt, int steps, double regularizer, int ngroups,
+                     gprx_batch* const* batches, const int* slots, int G, const int* vw_idx1, int T,
+                     const int* traj_group, const double* start, double* final_state, double* proj_err,
+                     int* status);
+
 /* ---- host-side CState helpers (bit-exact copies) ------------------------------------------ */
 /* out[13*b + 0..12] = [xc(3), qc.w, qc.x, qc.y, qc.z, vc(3), wc(3)] for body b (CState.jl:20,26) */
 int gprx_cstate_pack(int nbodies, const double* xc, const double* qc_wxyz, const double* vc,

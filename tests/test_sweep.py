@@ -64,8 +64,33 @@ def test_reduced_sweep_against_oracle(ctx, mech):
                     ok, info = _mll_ok(r["mll"][t, g], trials[t]["X"], np.atleast_2d(trials[t]["Y"])[g],
                                        r["theta"][t, g], mode)
                     assert ok, (mech, N, var, t, g, info)
-            if var == "max":
+            if var == "max":  # device predictdynamics (projectv! + updatestate!) against the oracle loop
+                from oracle import projection_oracle as PO
+
                 assert np.sum(np.isfinite(r["kstep_mse"])) >= TRIALS // 2, (mech, N, r["status"])
+                idx = data.VW_INDICES[mech]
+                for t in ((0,) if N == SIZES[1] else ()):  # one size: the oracle loop is slow Python
+                    if not (np.all(r["status"][t] == 0) and np.isfinite(r["kstep_mse"][t])):
+                        continue
+                    tr = trials[t]
+                    truth = data.test_truth(mech, TESTS, tr["seed"], STEPS)["X"].T
+
+                    def kerr_max(md):
+                        al = [O.fit(tr["X"], tr["Y"][g], r["theta"][t, g], None, md)["alpha"] for g in range(G)]
+                        pars = [O.kernel_params(r["theta"][t, g], tr["X"].shape[0]) for g in range(G)]
+
+                        def predict(obs):
+                            D = O.dist_stack(tr["X"], obs[:, None], md)
+                            return np.array([(pars[g][1] * np.exp(-O.weighted_r(D, pars[g][0]) * 0.5))[:, 0] @ al[g]
+                                             for g in range(G)])
+
+                        fin = [PO.predictdynamics(mech, predict, tr["Xs"][:, m], STEPS, idx,
+                                                  regularizer=1e-10 if mech == "FB" else 0.0)[0] for m in range(TESTS)]
+                        return data.position_mse(truth, np.stack(fin))
+
+                    e_ref, e_alt = kerr_max(mode), kerr_max(1 - mode)
+                    tol = max(1e-8 * max(1.0, abs(e_ref)), 10 * abs(e_ref - e_alt))
+                    assert abs(r["kstep_mse"][t] - e_ref) <= tol, (mech, N, t, r["kstep_mse"][t], e_ref, tol)
                 continue
             usesin = var == "min_sin"
             nc = NCOORD[mech]
