@@ -5,7 +5,7 @@
 // (LBFGS: m = 10, alphaguess InitialStatic(alpha = 1), scaleinvH0, twoloop!, update_h!,
 // assess_convergence with g_abstol = 1e-8, x_abstol = f_abstol = 0, successive_f_tol = 1 and
 // the non-finite-gradient break) and LineSearches 7.1.1
-// (BackTracking order 2: c_1 = 1e-4, rho_hi = 0.5, rho_lo = 0.1, iterfinite from 1) -- [ext, not in
+// (BackTracking order 2: c_1 = 1e-4, rho_hi = 0.5, rho_lo = 0.1, iterfinite from 0) -- [ext, not in
 // the reference tree; Manifest.toml pins the versions].  The host restatement of the same
 // algorithm is gpr.jl_amd/gprx/optim.py (lbfgs_steps / BackTracking.search); this kernel is its
 // state machine, one thread per slot, so a whole batch's optimisers advance in lock-step between
@@ -163,7 +163,8 @@ __global__ __launch_bounds__(64) void k_lbfgs(LbArgs a, DevBatch db, int init) {
     bool want = false, want_g = false;  // request issued by this step: point in v.xr
     int resume = PH_DONE;
     switch (ph) {
-      case PH_START:
+      case PH_START:  // value_gradient!!: one f and one g call
+        I[I_FCALLS] += 1;
         I[I_GCALLS] += 1;
         want = want_g = true;
         for (int j = 0; j < n; ++j) v.xr[j] = v.x[j];
@@ -210,7 +211,7 @@ __global__ __launch_bounds__(64) void k_lbfgs(LbArgs a, DevBatch db, int init) {
       case PH_LS_FIRST:
         S[D_PHIX0] = S[D_PHI0];
         S[D_PHIX1] = S[D_CF];
-        I[I_ITFIN] = 1;
+        I[I_ITFIN] = 0;
         I[I_PH] = PH_LS_FIN;
         break;
       case PH_LS_FIN:
@@ -242,7 +243,7 @@ __global__ __launch_bounds__(64) void k_lbfgs(LbArgs a, DevBatch db, int init) {
             I[I_PH] = PH_STEP;
             break;
           }
-          double atmp = -(dphi0 * a2 * a2) / (2.0 * (phix1 - phi0 - dphi0 * a2));
+          double atmp = -(dphi0 * (a2 * a2)) / (2.0 * (phix1 - phi0 - dphi0 * a2));  // dphi_0 * a2^2
           atmp = nanmin_(atmp, a2 * a.rho_hi);
           S[D_A1] = a2;
           S[D_A2] = nanmax_(atmp, a2 * a.rho_lo);
@@ -315,6 +316,7 @@ __global__ __launch_bounds__(64) void k_lbfgs(LbArgs a, DevBatch db, int init) {
         else if (I[I_FCNT] > a.successive_f_tol) I[I_STOP] = LB_STOP_F_TOL, I[I_CONV] = 1;
         if (I[I_CONV]) I[I_PH] = PH_DONE;
         else if (a.time_up) I[I_STOP] = LB_STOP_TIME_LIMIT, I[I_PH] = PH_DONE;
+        else if (capped && I[I_FCALLS] >= a.max_evals) I[I_STOP] = LB_STOP_MAX_EVALS, I[I_PH] = PH_DONE;  // f_calls_limit
         else if (!gfin) I[I_STOP] = LB_STOP_NAN_GRADIENT, I[I_PH] = PH_DONE;
         else I[I_PH] = PH_ITER;
         break;
@@ -324,13 +326,6 @@ __global__ __launch_bounds__(64) void k_lbfgs(LbArgs a, DevBatch db, int init) {
         break;
     }
     if (!want) continue;
-    // deterministic evaluation budget: counted at request time, as lbfgs_steps' budget()
-    if (capped && I[I_FCALLS] + I[I_GCALLS] > a.max_evals) {
-      I[I_STOP] = LB_STOP_MAX_EVALS;
-      I[I_CONV] = 0;
-      I[I_PH] = PH_DONE;
-      break;
-    }
     I[I_RESUME] = resume;
     bool hit = I[I_CVALID] != 0;
     for (int j = 0; j < n && hit; ++j) hit = v.cx[j] == v.xr[j];

@@ -8,7 +8,7 @@
  * "key v1 v2 ..." lines with %.17g:
  *   single GP on Y row 0 (GP / update_target_and_dtarget! / predict_f):  mll, grad, mu, var
  *   the G outputs of the trial as one batch (one gprx_batch_run):        batch_mll
- *   optimize! of every output on the device, 15-evaluation budget:       opt_min, opt_evals,
+ *   optimize! of every output on the device, f_calls_limit 15:             opt_min, opt_evals,
  *                                                                        opt_theta0 (slot 0)
  * Exit status 0 on success; on failure the gprx status string goes to stderr.
  */
@@ -115,7 +115,7 @@ int main(int argc, char** argv) {
   int rounds = 0;
   rc = gprx_batch_optimize(b, th, &opt, thx, fmin, NULL, fc, gc, NULL, &rounds);
   if (rc) return fail("gprx_batch_optimize", rc, ctx);
-  for (int g = 0; g < G; ++g) ev[g] = fc[g] + gc[g];
+  for (int g = 0; g < G; ++g) ev[g] = fc[g];  /* f calls = device evaluations (Optim f_calls_limit) */
   print_row("opt_min", fmin, G);
   print_row("opt_evals", ev, G);
   print_row("opt_theta0", thx, d + 2);

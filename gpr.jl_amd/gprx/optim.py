@@ -13,9 +13,13 @@ x_abstol = f_abstol = 0, i.e. an exact repeat of x stops, and an exact repeat of
 has happened on successive_f_tol + 1 = 2 successive iterations; allow_f_increases = true); a
 failed line search moves x by the search's last step and stops before the gradient evaluation;
 a non-finite gradient after an iteration ends the loop ("Terminated early due to NaN in
-gradient").
+gradient").  Calls are counted as NLSolversBase does: the initial value_gradient!! is one f and
+one g call, every line-search trial one f call, update_g! one g call.
 Besides the reference's wall-clock cap, `max_evals` gives the deterministic evaluation budget
-SURVEY.md section 8d asks for.  `gprx.batch.GPBatch.optimize` runs the same algorithm on the
+SURVEY.md section 8d asks for: Optim's own Options.f_calls_limit, a soft limit checked after each
+iteration (f calls = the initial evaluation + every line-search trial = the device evaluations of
+the lock-step driver, whose evaluations all carry the gradient).  The independent restatement in
+oracle/lbfgs_oracle.py checks this one.  `gprx.batch.GPBatch.optimize` runs the same algorithm on the
 device (k_lbfgs), one lock-step round per batch evaluation.
 """
 from __future__ import annotations
@@ -47,7 +51,7 @@ class BackTracking:
         iterfinitemax = -math.log2(np.finfo(float).eps)
         a1 = a2 = alpha_0
         phix0, phix1 = phi_0, (yield a1)
-        it_fin = 1  # LineSearches: iterfinite = 1, so at most iterfinitemax - 1 halvings
+        it_fin = 0  # LineSearches BackTracking: iterfinite = 0, at most iterfinitemax halvings
         while not math.isfinite(phix1) and it_fin < iterfinitemax:
             it_fin += 1
             a1 = a2
@@ -61,7 +65,7 @@ class BackTracking:
             if it > self.iterations:
                 raise LineSearchError(a2, phix1)
             if self.order == 2 or it == 1:
-                atmp = _div(-(dphi_0 * a2 * a2), 2 * (phix1 - phi_0 - dphi_0 * a2))
+                atmp = _div(-(dphi_0 * (a2 * a2)), 2 * (phix1 - phi_0 - dphi_0 * a2))  # Julia: dphi_0 * a2^2
             else:
                 div = _div(1.0, a1 * a1 * a2 * a2 * (a2 - a1))
                 a = (a1 * a1 * (phix1 - phi_0 - dphi_0 * a2) - a2 * a2 * (phix0 - phi_0 - dphi_0 * a1)) * div
@@ -133,7 +137,7 @@ class Options:
     g_abstol: float = 1e-8
     time_limit: float = math.nan
     successive_f_tol: int = 1
-    max_evals: int | None = None  # deterministic budget (not in Optim)
+    max_evals: int | None = None  # Optim's f_calls_limit: a soft limit on f calls
 
 
 @dataclass
@@ -145,10 +149,6 @@ class Result:
     g_calls: int
     converged: bool
     stopped_by: str
-
-
-class _Budget(Exception):
-    pass
 
 
 def _twoloop(g, rho, dxh, dgh, m, pseudo_it, scaleinvH0):
@@ -198,8 +198,6 @@ def lbfgs_steps(x0, method: LBFGS | None = None, options: Options | None = None)
 
     def budget(kind):
         calls[kind] += 1
-        if options.max_evals is not None and calls["f"] + calls["g"] > options.max_evals:
-            raise _Budget()
 
     x = np.array(x0, dtype=np.float64)
     n = x.shape[0]
@@ -212,76 +210,76 @@ def lbfgs_steps(x0, method: LBFGS | None = None, options: Options | None = None)
     fx = math.nan
     converged = False
     counter_f_tol = 0
-    try:
+    budget("f")  # value_gradient!!: one f and one g call
+    budget("g")
+    fx, g = yield ("fg", x)
+    pseudo = 0
+    converged = bool(np.max(np.abs(g)) <= options.g_abstol)
+    if converged:
+        stopped = "g_tol"
+    while not converged and it < options.iterations:
+        it += 1
+        pseudo += 1
+        s = _twoloop(g, rho, dxh, dgh, m, pseudo, method.scaleinvH0)
+        g_prev = g.copy()
+        dphi0 = _dot(g, s)
+        if dphi0 >= 0:  # reset_search_direction!
+            pseudo = 1
+            s = -g
+            dphi0 = _dot(g, s)
+        ls = method.linesearch.search(method.alphaguess, fx, dphi0)
+        try:
+            a = next(ls)
+            while True:
+                budget("f")
+                a = ls.send((yield ("f", x + a * s)))
+        except StopIteration as e:
+            alpha, ls_ok = e.value[0], True
+        except LineSearchError as e:
+            alpha, ls_ok, ls_phi = e.alpha, False, e.phi
+        dx = alpha * s
+        x_prev, f_prev = x, fx
+        x = x + dx
+        if not ls_ok:
+            # Optim's update_state! reports the failed search and the loop breaks before
+            # update_g!: x has moved, the objective's value cache holds phi(alpha)
+            fx = float(ls_phi)
+            stopped = "linesearch"
+            break
         budget("g")
         fx, g = yield ("fg", x)
-        pseudo = 0
-        converged = bool(np.max(np.abs(g)) <= options.g_abstol)
+        dg = g - g_prev
+        denom = _dot(dx, dg)
+        r = _div(1.0, denom)
+        if not math.isinf(r):
+            i = (pseudo - 1) % m
+            dxh[i] = dx.copy()
+            dgh[i] = dg.copy()
+            rho[i] = r
+        # assess_convergence with Optim's defaults x_tol = f_tol = 0 (exact repeats) and g_tol;
+        # f convergence counts only on successive iterations (Options.successive_f_tol)
+        with np.errstate(invalid="ignore"):
+            g_conv = bool(np.max(np.abs(g)) <= options.g_abstol)
+            x_conv = bool(np.max(np.abs(x - x_prev)) <= 0.0)
+            f_conv = bool(abs(fx - f_prev) <= 0.0)
+        counter_f_tol = counter_f_tol + 1 if f_conv else 0
+        if g_conv:
+            converged, stopped = True, "g_tol"
+        elif x_conv:
+            converged, stopped = True, "x_tol"
+        elif counter_f_tol > options.successive_f_tol:
+            converged, stopped = True, "f_tol"
         if converged:
-            stopped = "g_tol"
-        while not converged and it < options.iterations:
-            it += 1
-            pseudo += 1
-            s = _twoloop(g, rho, dxh, dgh, m, pseudo, method.scaleinvH0)
-            g_prev = g.copy()
-            dphi0 = _dot(g, s)
-            if dphi0 >= 0:  # reset_search_direction!
-                pseudo = 1
-                s = -g
-                dphi0 = _dot(g, s)
-            ls = method.linesearch.search(method.alphaguess, fx, dphi0)
-            try:
-                a = next(ls)
-                while True:
-                    budget("f")
-                    a = ls.send((yield ("f", x + a * s)))
-            except StopIteration as e:
-                alpha, ls_ok = e.value[0], True
-            except LineSearchError as e:
-                alpha, ls_ok, ls_phi = e.alpha, False, e.phi
-            dx = alpha * s
-            x_prev, f_prev = x, fx
-            x = x + dx
-            if not ls_ok:
-                # Optim's update_state! reports the failed search and the loop breaks before
-                # update_g!: x has moved, the objective's value cache holds phi(alpha)
-                fx = float(ls_phi)
-                stopped = "linesearch"
-                break
-            budget("g")
-            fx, g = yield ("fg", x)
-            dg = g - g_prev
-            denom = _dot(dx, dg)
-            r = _div(1.0, denom)
-            if not math.isinf(r):
-                i = (pseudo - 1) % m
-                dxh[i] = dx.copy()
-                dgh[i] = dg.copy()
-                rho[i] = r
-            # assess_convergence with Optim's defaults x_tol = f_tol = 0 (exact repeats) and g_tol;
-            # f convergence counts only on successive iterations (Options.successive_f_tol)
-            with np.errstate(invalid="ignore"):
-                g_conv = bool(np.max(np.abs(g)) <= options.g_abstol)
-                x_conv = bool(np.max(np.abs(x - x_prev)) <= 0.0)
-                f_conv = bool(abs(fx - f_prev) <= 0.0)
-            counter_f_tol = counter_f_tol + 1 if f_conv else 0
-            if g_conv:
-                converged, stopped = True, "g_tol"
-            elif x_conv:
-                converged, stopped = True, "x_tol"
-            elif counter_f_tol > options.successive_f_tol:
-                converged, stopped = True, "f_tol"
-            if converged:
-                break
-            if not math.isnan(options.time_limit) and time.time() - t0 > options.time_limit:
-                stopped = "time_limit"
-                break
-            if not np.all(np.isfinite(g)):
-                stopped = "nan_gradient"
-                break
-    except _Budget:
-        stopped = "max_evals"
-        converged = False
+            break
+        if not math.isnan(options.time_limit) and time.time() - t0 > options.time_limit:
+            stopped = "time_limit"
+            break
+        if options.max_evals is not None and calls["f"] >= options.max_evals:  # f_calls_limit
+            stopped = "max_evals"
+            break
+        if not np.all(np.isfinite(g)):
+            stopped = "nan_gradient"
+            break
     return Result(x, float(fx), it, calls["f"], calls["g"], converged, stopped)
 
 

@@ -143,7 +143,9 @@ int gprx_batch_alpha(gprx_batch* batch, double* alpha);
 typedef struct gprx_opt_options {
   int m;              /* LBFGS history length (Optim: 10)                                        */
   int iterations;     /* Options.iterations (1000)                                               */
-  int max_evals;      /* deterministic budget of f + g evaluations per slot; < 0: none (default)  */
+  int max_evals;      /* Options.f_calls_limit, the deterministic budget: a soft limit on f calls
+                         (the initial evaluation + every line-search trial = the device evaluations),
+                         checked after each iteration; < 0: none (default)                        */
   int ls_iterations;  /* BackTracking.iterations (1000)                                          */
   int scaleinvH0;     /* LBFGS scaleinvH0 (true)                                                 */
   int refit;          /* 1: end with one evaluation of every slot at its minimiser, as optimize!

