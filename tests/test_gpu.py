@@ -13,6 +13,10 @@ formulations already differ by up to 7.5e-10 in the LML.
   grad  |d| <= max(1e-7 * max(1, max|grad|),    10 spread)
   mu    |d| <= max(1e-9 * max|y|,               10 spread)
   var   |d| <= max(1e-9 * sf^2,                 10 spread)
+The LML bound is 1e-10 relative, flat, on the well-conditioned P2 and FB inputs (SURVEY.md 8(d);
+measured: <= 1.8e-11 on the golden P2/FB cases in both modes, ~1e-14 at the full P2 N=2048 and FB
+N=4096 sizes).  The adaptive bound above is kept only for the cartpole and pendulum inputs, whose
+cond(K) puts the oracle's own two formulations up to 7.5e-10 apart.
 Status / pivot index / CState indexing: exact.
 """
 import math
@@ -25,27 +29,30 @@ pytestmark = pytest.mark.gpu
 from oracle import gp_oracle as O  # noqa: E402
 
 TOL_MLL, TOL_GRAD, TOL_MU, TOL_VAR = 1e-9, 1e-7, 1e-9, 1e-9
+TOL_MLL_STRICT = 1e-10  # P2 / FB (well-conditioned): flat, no adaptive term
+STRICT = ("p2", "fb")
 DEFAULT_MODE = 1  # GPRX_DIST_DIRECT, the library default
 
 
-def tolerances(f, f2, y, theta):
+def tolerances(f, f2, y, theta, strict=False):
     """Per-quantity bounds for a result compared against oracle fit f (f2: the same fit in the
-    other distance mode)."""
+    other distance mode).  strict: the flat 1e-10 LML bound of the well-conditioned mechanisms."""
     def spread(k):
         return float(np.max(np.abs(np.asarray(f[k]) - np.asarray(f2[k])))) if k in f and k in f2 else 0.0
 
     sf2 = math.exp(2 * theta[-1])
+    mll_adaptive = max(TOL_MLL * max(1.0, abs(f["mll"])), 10 * spread("mll"), 10 * float(f.get("mll_sens", 0.0)))
     return dict(
-        mll=max(TOL_MLL * max(1.0, abs(f["mll"])), 10 * spread("mll"), 10 * float(f.get("mll_sens", 0.0))),
+        mll=TOL_MLL_STRICT * max(1.0, abs(f["mll"])) if strict else mll_adaptive,
         grad=max(TOL_GRAD * max(1.0, float(np.max(np.abs(f["grad"])))), 10 * spread("grad")),
         mu=max(TOL_MU * float(np.max(np.abs(y))), 10 * spread("mu")),
         var=max(TOL_VAR * sf2, 10 * spread("var")),
     )
 
 
-def check_slot(r, s, X, y, theta, Xs, mode):
+def check_slot(r, s, X, y, theta, Xs, mode, strict=False):
     f = O.fit(X, y, theta, Xs, mode)
-    t = tolerances(f, O.fit(X, y, theta, Xs, 1 - mode), y, theta)
+    t = tolerances(f, O.fit(X, y, theta, Xs, 1 - mode), y, theta, strict)
     assert r["status"][s] == 0
     assert abs(r["mll"][s] - f["mll"]) <= t["mll"]
     if r["grad"] is not None:
@@ -86,7 +93,7 @@ def test_golden_batch(gprx, ctx, golden_dir, name, mode):
     for g in range(G):
         f = {k: z[f"{k}_{tag}"][g] for k in ("mll", "grad", "mu", "var")}
         f2 = {k: z[f"{k}_{other}"][g] for k in ("mll", "grad", "mu", "var")}
-        t = tolerances(f, f2, Y[g], th)
+        t = tolerances(f, f2, Y[g], th, name.startswith(STRICT))
         assert abs(r["mll"][g] - f["mll"]) <= t["mll"]
         assert np.max(np.abs(r["grad"][g] - f["grad"])) <= t["grad"]
         assert np.max(np.abs(r["mu"][g] - f["mu"])) <= t["mu"]
@@ -126,7 +133,7 @@ def test_full_size_p2_against_oracle_and_determinism(gprx, ctx):
     b.set_test(tr["Xs"])
     r1 = b.run(np.tile(th, (B, 1)), grad=True, predict=True)
     r2 = b.run(np.tile(th, (B, 1)), grad=True, predict=True)
-    check_slot(r1, 0, tr["X"], tr["Y"][0], th, tr["Xs"], ctx.dist_mode)
+    check_slot(r1, 0, tr["X"], tr["Y"][0], th, tr["Xs"], ctx.dist_mode, strict=True)
     for k in ("mll", "grad", "mu", "var"):
         np.testing.assert_array_equal(r1[k], r2[k])
         for s in range(1, B):
@@ -168,7 +175,7 @@ def test_gpe_mirror_api(gprx, ctx, golden_dir):
     gp = gprx.GP(X, y, mean, gprx.SEArd(th[1:-1], th[-1]), ctx=ctx)
     mu0 = np.array([0.1 * X[8, t] for t in range(X.shape[1])])
     f = O.fit(X, y - mu0, th, Xs, ctx.dist_mode)
-    assert abs(gp.mll - f["mll"]) <= TOL_MLL * abs(f["mll"])
+    assert abs(gp.mll - f["mll"]) <= TOL_MLL_STRICT * abs(f["mll"])
     gp.update_mll_and_dmll()
     assert np.max(np.abs(gp.dmll - f["grad"])) <= TOL_GRAD * np.max(np.abs(f["grad"]))
     mu_y, var_y = gprx.predict_y(gp, Xs)
@@ -207,7 +214,7 @@ def test_device_pointer_inputs(gprx, ctx, golden_dir):
     b.set_test_device(Xsd.data_ptr(), Xs.shape[1], 0)
     r = b.run(np.tile(th, (G, 1)), grad=True, predict=True)
     tag = "exp" if ctx.dist_mode == 0 else "dir"
-    np.testing.assert_allclose(r["mll"], z[f"mll_{tag}"], rtol=TOL_MLL)
+    np.testing.assert_allclose(r["mll"], z[f"mll_{tag}"], rtol=TOL_MLL_STRICT)
     np.testing.assert_allclose(r["mu"], z[f"mu_{tag}"], rtol=0, atol=TOL_MU * np.max(np.abs(Y)))
 
 
@@ -222,7 +229,7 @@ def test_gpu_evaluator_for_sharding(gprx, ctx, golden_dir):
     tag = "exp" if ctx.dist_mode == 0 else "dir"
     assert r["mll"].shape == (2, G) and r["mu"].shape == (2, G, z["Xs"].shape[1])
     for t in range(2):
-        np.testing.assert_allclose(r["mll"][t], z[f"mll_{tag}"], rtol=TOL_MLL)
+        np.testing.assert_allclose(r["mll"][t], z[f"mll_{tag}"], rtol=TOL_MLL_STRICT)
     np.testing.assert_array_equal(r["mll"][0], r["mll"][1])
 
 
@@ -290,7 +297,7 @@ def test_factorisation_paths_match_golden(gprx, golden_dir, leaf, small_n):
         assert np.all(r["status"] == 0)
         t = "exp" if c.dist_mode == 0 else "dir"
         for g in range(G):
-            assert abs(r["mll"][g] - z[f"mll_{t}"][g]) <= TOL_MLL * max(1.0, abs(z[f"mll_{t}"][g]))
+            assert abs(r["mll"][g] - z[f"mll_{t}"][g]) <= TOL_MLL_STRICT * max(1.0, abs(z[f"mll_{t}"][g]))
             gs = max(1.0, np.max(np.abs(z[f"grad_{t}"][g])))
             assert np.max(np.abs(r["grad"][g] - z[f"grad_{t}"][g])) <= TOL_GRAD * gs
             assert np.max(np.abs(r["mu"][g] - z[f"mu_{t}"][g])) <= TOL_MU * np.max(np.abs(Y[g]))
@@ -337,7 +344,7 @@ def test_production_path_b32_full_size(gprx, ctx):
         assert np.all(np.isfinite(r1[k]))
         np.testing.assert_array_equal(r1[k], r2[k])
     for s in (0, 13, 31):
-        check_slot(r1, s, X[s], Y[s], T[s], Xs[s], ctx.dist_mode)
+        check_slot(r1, s, X[s], Y[s], T[s], Xs[s], ctx.dist_mode, strict=True)
     b.close()
 
 
@@ -368,8 +375,10 @@ def test_mean_only_prediction_matches_full(gprx, ctx, golden_dir):
 def test_fb_full_size_n4096_d52(gprx, ctx):
     """BASELINE config FB: N=4096, d=52, the 12 per-output GPs of one trial with a theta-independent
     prior mean subtracted (MeanDynamics role), M=100 test states.  Two slots against the oracle
-    (mll, gradient, mean, variance; the LML bound uses the oracle's rounding sensitivity), every
-    slot finite and bit-identical across repeated runs."""
+    (mll to the flat 1e-10 relative bound, gradient, mean, variance), every slot finite and
+    bit-identical across repeated runs.  The prior mean 0.05 x[8] is synthetic: the experiments'
+    MeanDynamics physics is out of scope, and any theta-independent mean enters the
+    device path the same way, as y - mu(X)."""
     from gprx import data
 
     tr = data.make_trial("FB", 4096, 100, seed=data.trial_seed("FB", 0))
@@ -389,7 +398,7 @@ def test_fb_full_size_n4096_d52(gprx, ctx):
         np.testing.assert_array_equal(r1[k], r2[k])
     for s in (0, 7):
         f = O.fit(tr["X"], Y[s], th, tr["Xs"], ctx.dist_mode)
-        assert abs(r1["mll"][s] - f["mll"]) <= max(TOL_MLL * abs(f["mll"]), 10 * f["mll_sens"])
+        assert abs(r1["mll"][s] - f["mll"]) <= TOL_MLL_STRICT * abs(f["mll"])
         assert np.max(np.abs(r1["grad"][s] - f["grad"])) <= TOL_GRAD * max(1.0, np.max(np.abs(f["grad"])))
         assert np.max(np.abs(r1["mu"][s] - f["mu"])) <= TOL_MU * np.max(np.abs(Y[s]))
         assert np.max(np.abs(r1["var"][s] - f["var"])) <= TOL_VAR * math.exp(2 * th[-1])
