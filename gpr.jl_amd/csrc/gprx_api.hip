@@ -66,6 +66,7 @@ struct gprx_batch {
   double* h_mu = nullptr;      // pinned, B*Mpad
   double* h_var = nullptr;
   int* h_status = nullptr;  // pinned, 2B (status, info)
+  int* opt_active = nullptr;  // device, B: the optimiser's per-round evaluation mask (DevBatch::active)
   bool factored = false;
   bool have_train = false;
   bool have_test = false;
@@ -485,6 +486,7 @@ int gprx_batch_create(gprx_ctx* c, int B, int d, int N, int M_max, gprx_batch** 
   if ((rc = dalloc(b, &db.status, 2 * Bs))) return fail(rc);
   db.info = db.status + Bs;
   if ((rc = dalloc(b, &db.lauum_order, 6 * (size_t)db.nlj))) return fail(rc);
+  if ((rc = dalloc(b, &b->opt_active, Bs))) return fail(rc);
   {
     std::vector<int> ord(6 * (size_t)db.nlj);
     gprx::lauum_order_host(db.nt, ord.data());
@@ -761,16 +763,23 @@ int gprx_batch_optimize(gprx_batch* b, const double* theta0, const gprx_opt_opti
   a.theta0 = th0d;
   a.result = th0d + (size_t)B * n;
   a.iws = (int*)(a.result + rd);
-  a.active = a.iws + (size_t)B * gprx::LB_NI;
-  a.result_i = a.active + B;
+  // the optimisers' activity flags double as the evaluation mask of the rounds (finished slots are
+  // skipped by every kernel); a per-batch buffer, so the captured round graph is reused across calls
+  a.active = b->opt_active;
+  a.result_i = a.iws + (size_t)B * gprx::LB_NI + B;
   double* h_res = (double*)hbuf;
   int* h_act = (int*)(h_res + rd);
   int* h_ri = h_act + B;
   // theta, L and the factorisation flags are overwritten from here on: the batch holds no valid
   // factorisation until the refit below has succeeded for every slot
   b->factored = false;
+  struct Unmask {  // every exit path evaluates all slots again
+    DevBatch& db;
+    ~Unmask() { db.active = nullptr; }
+  } um{db};
   HIPCHK(c, hipMemcpyAsync(th0d, theta0, (size_t)B * n * sizeof(double), hipMemcpyHostToDevice, c->stream));
   gprx::launch_lbfgs(a, db, 1, c->stream);
+  db.active = a.active;
   const auto t0 = std::chrono::steady_clock::now();
   int nr = 0;
   for (;;) {
@@ -790,6 +799,7 @@ int gprx_batch_optimize(gprx_batch* b, const double* theta0, const gprx_opt_opti
   }
   HIPCHK(c, hipMemcpyAsync(h_res, a.result, rd * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipMemcpyAsync(h_ri, a.result_i, (size_t)B * 4 * sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  db.active = nullptr;
   if (o.refit) {  // optimize!: set_params!(gp, minimizer); update_target!(gp)
     gprx::launch_lbfgs_final(a, db, c->stream);
     int rc = run_eval(b, true, false, true);

@@ -62,6 +62,8 @@ struct DevBatch {
   int* status;                 // B
   int* info;                   // B
   int* lauum_order;            // nlj x 6: two (first row, first column, unit id) per job, long + short
+  const int* active;           // B or null: evaluate only the slots with active[s] != 0 (the device
+                               //   optimiser's rounds; null = every slot)
 };
 
 // GEMM operations of the recursive factorisation / inverse / prediction (tile units, see
