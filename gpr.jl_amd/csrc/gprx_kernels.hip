@@ -540,11 +540,9 @@ __device__ __forceinline__ void diag_tile_fast(const DevBatch& db, int slot, int
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, lr = l & 15, lk = l >> 4;
   const size_t ld = db.ld;
   const double* A = db.K + (size_t)slot * db.mat + (size_t)jt * TS * ld + jt * TS;
-#pragma unroll
-  for (int i = 0; i < TS * TS / NTHR; ++i) {
-    const int e = tid + i * NTHR, r = e & 63, c = e >> 6;
-    const double v = A[(size_t)c * ld + r];  // unconditional (inside the tile): all 16 loads in flight at once
-    T[c * FS + r] = (r >= c) ? v : 0.0;
+  for (int e = tid; e < TS * TS; e += NTHR) {
+    const int r = e & 63, c = e >> 6;
+    T[c * FS + r] = (r >= c) ? A[(size_t)c * ld + r] : 0.0;
     Xi[c * FS + r] = 0.0;
   }
   __syncthreads();

@@ -50,6 +50,13 @@ __device__ __forceinline__ bool map_block(int bid, int B, int T, int& slot, int&
   return slot < B;
 }
 
+// ... and the slot's evaluation mask: db.active (optional, device) lets the optimiser's rounds skip
+// the slots whose optimisers have finished (every workgroup of such a slot returns at once)
+__device__ __forceinline__ bool slot_active(const DevBatch& db, int slot) { return !db.active || db.active[slot] != 0; }
+__device__ __forceinline__ bool map_slot(const DevBatch& db, int T, int& slot, int& unit) {
+  return map_block(blockIdx.x, db.B, T, slot, unit) && slot_active(db, slot);
+}
+
 // Units of a tile-pair decomposition.  rect R x C: pairs of rows per column; lower triangle of
 // R x R: column c holds rows c..R-1.
 __host__ __device__ inline int pair_units(int R, int C, bool tri) {
@@ -400,7 +407,7 @@ __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
   double* xj = sm + d * TS;
   double* pw = sm + 2 * d * TS;
   int slot, t, i = 0, j = 0;
-  if (!map_block(blockIdx.x, db.B, db.ntl, slot, t)) return;
+  if (!map_slot(db, db.ntl, slot, t)) return;
   {  // t-th lower tile in column-major order
     int c = 0, u = t;
     while (u >= db.nt - c) {
@@ -522,7 +529,9 @@ __global__ __launch_bounds__(NTHR) void k_center(DevBatch db) {
 // D lane l reg q = D[(l>>4) + 4q][l&15].
 // ============================================================================================
 __device__ __forceinline__ void diag_tile_fast(const DevBatch& db, int slot, int jt);
-__global__ __launch_bounds__(NTHR) void k_diag_f(DevBatch db, int jt) { diag_tile_fast(db, blockIdx.x, jt); }
+__global__ __launch_bounds__(NTHR) void k_diag_f(DevBatch db, int jt) {
+  if (slot_active(db, blockIdx.x)) diag_tile_fast(db, blockIdx.x, jt);
+}
 constexpr int FS = TS + 1;  // LDS column stride of the tile images
 __device__ __forceinline__ void diag_tile_fast(const DevBatch& db, int slot, int jt) {
   __shared__ double T[TS * FS];   // T[c*FS + r] = A[r][c], then L (lower)
@@ -531,9 +540,11 @@ __device__ __forceinline__ void diag_tile_fast(const DevBatch& db, int slot, int
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, lr = l & 15, lk = l >> 4;
   const size_t ld = db.ld;
   const double* A = db.K + (size_t)slot * db.mat + (size_t)jt * TS * ld + jt * TS;
-  for (int e = tid; e < TS * TS; e += NTHR) {
-    const int r = e & 63, c = e >> 6;
-    T[c * FS + r] = (r >= c) ? A[(size_t)c * ld + r] : 0.0;
+#pragma unroll
+  for (int i = 0; i < TS * TS / NTHR; ++i) {
+    const int e = tid + i * NTHR, r = e & 63, c = e >> 6;
+    const double v = A[(size_t)c * ld + r];  // unconditional (inside the tile): all 16 loads in flight at once
+    T[c * FS + r] = (r >= c) ? v : 0.0;
     Xi[c * FS + r] = 0.0;
   }
   __syncthreads();
@@ -811,7 +822,7 @@ __device__ __forceinline__ void gemm_body(const DevBatch& db, const GemmGeom& g1
   op_rect(g2, db.nt, db.mt, r02, c02, R2, C2, tri2);
   const int T1 = op_units(g1, db.nt, db.mt), T2 = g2.op == OP_NONE ? 0 : op_units(g2, db.nt, db.mt);
   int slot, u, pr, pc;
-  if (!map_block(blockIdx.x, db.B, T1 + T2, slot, u)) return;
+  if (!map_slot(db, T1 + T2, slot, u)) return;
   const GemmGeom g = u < T1 ? g1 : g2;  // block-uniform
   if (u >= T1) {
     u -= T1;
@@ -899,7 +910,7 @@ __device__ __forceinline__ void gemm_body_pair(const DevBatch& db, const GemmGeo
   op_rect(g2, db.nt, db.mt, r02, c02, R2, C2, tri2);
   const int T1 = pair_op_units(g1, db.nt, db.mt), T2 = g2.op == OP_NONE ? 0 : pair_op_units(g2, db.nt, db.mt);
   int slot, u, pr, pc;
-  if (!map_block(blockIdx.x, db.B, T1 + T2, slot, u)) return;
+  if (!map_slot(db, T1 + T2, slot, u)) return;
   const GemmGeom g = u < T1 ? g1 : g2;  // block-uniform
   if (u >= T1) {
     u -= T1;
@@ -1090,6 +1101,7 @@ __device__ __forceinline__ void leaf_body(const DevBatch& db, int o, int n) {
   // one 64 x 64 tile task per wave (4 at a time); tile stores through the wave's LDS buffer
   __shared__ double tbs[4 * 16 * (TS + 1)];
   const int slot = blockIdx.x;
+  if (!slot_active(db, slot)) return;
   const int w = threadIdx.x >> 6;
   double* tb = tbs + w * 16 * (TS + 1);
   const size_t ld = db.ld, so = (size_t)slot * db.mat;
@@ -1186,7 +1198,7 @@ __global__ __launch_bounds__(NTHR) void k_leaf(DevBatch db, int o, int n) { leaf
 __global__ __launch_bounds__(NTHR) void k_alpha(DevBatch db, int phase) {
   __shared__ double part[4][TS];
   int slot, i;
-  if (!map_block(blockIdx.x, db.B, db.nt, slot, i)) return;
+  if (!map_slot(db, db.nt, slot, i)) return;
   const int r = threadIdx.x & 63, pt = threadIdx.x >> 6;
   if (phase == 0) {  // z = L^-1 y from the producers' partials: rows of tile i, halves h < 2(i+1)
     double acc = 0.0;
@@ -1252,7 +1264,7 @@ constexpr int SPW = DMAX + 2;  // per-wave partial row: S_p (d), S_f, T
 __device__ __forceinline__ void lauum_unit(const DevBatch& db, int slot, int pr, int pc, int u);
 __device__ __forceinline__ void lauum_body(const DevBatch& db) {
   int slot, job;
-  if (!map_block(blockIdx.x, db.B, db.nlj, slot, job)) return;
+  if (!map_slot(db, db.nlj, slot, job)) return;
   const int* jb = db.lauum_order + 6 * job;
   lauum_unit(db, slot, jb[0], jb[1], jb[2]);
   if (jb[3] >= 0) {  // block-uniform: the folded short unit
@@ -1475,6 +1487,7 @@ void lauum_order_host(int nt, int* out) {
 __global__ __launch_bounds__(NTHR) void k_finalize(DevBatch db, int want_grad) {
   __shared__ double red[4];
   const int slot = blockIdx.x, tid = threadIdx.x, d = db.d;
+  if (!slot_active(db, slot)) return;
   const double* y = db.Y + (size_t)slot * db.Npad;
   const double* al = db.alpha + (size_t)slot * db.Npad;
   double s = 0.0;
@@ -1528,7 +1541,7 @@ __global__ __launch_bounds__(NTHR) void k_pred_cross(DevBatch db) {
   double* xs = sm + d * TS;
   double* pw = sm + 2 * d * TS;
   int slot, t;
-  if (!map_block(blockIdx.x, db.B, db.nt * db.mt, slot, t)) return;
+  if (!map_slot(db, db.nt * db.mt, slot, t)) return;
   const int ch = t / db.mt, mtile = t - ch * db.mt;
   const double* X = db.X + (size_t)slot * db.Npad * d;
   const double* Xq = db.Xs + (size_t)slot * db.Mpad * d;
@@ -1602,7 +1615,7 @@ __global__ __launch_bounds__(NTHR) void k_pred_cross(DevBatch db) {
 __global__ __launch_bounds__(NTHR) void k_pred_mu(DevBatch db) {
   __shared__ double part[2][NTHR];
   int slot, ch;
-  if (!map_block(blockIdx.x, db.B, db.nt, slot, ch)) return;
+  if (!map_slot(db, db.nt, slot, ch)) return;
   const double* KsT = db.KsT + ((size_t)slot * db.Npad + (size_t)ch * TS) * db.Mpad;
   const double* al = db.alpha + (size_t)slot * db.Npad + ch * TS;
   const int tid = threadIdx.x, h = tid >> 7, mm = tid & 127;
