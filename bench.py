@@ -214,6 +214,12 @@ def cpu_baseline(X, Y, T, XT, gpu=None, max_seconds: float = 15.0, max_fits: int
     return base, acc
 
 
+def _progress(rank: int, msg: str):
+    """One progress line on stderr (rank 0): the JSON result stays the only stdout line."""
+    if rank == 0:
+        print(f"bench: {msg}", file=sys.stderr, flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -261,11 +267,13 @@ def main():
         torch.cuda.synchronize()
 
     TH = T.reshape(rb.n, G, -1)  # per (local trial, output)
+    _progress(rank, f"{B} slots per rank, {world} rank(s); warm-up")
     for _ in range(args.warmup):
         r = rb.evaluate(TH)
     ok = bool(np.all(r["status"] == 0)) if args.warmup else True
 
     barrier()
+    _progress(rank, f"timing {args.steps} steps")
     t0 = time.perf_counter()
     for _ in range(args.steps):
         r = rb.evaluate(TH)
@@ -284,6 +292,7 @@ def main():
     roof = parts = None
     kern = {}
     if not args.no_prof:
+        _progress(rank, "per-kernel timing pass")
         ctx.set_profiling(True)
         ctx.reset_stats()
         nprof = max(1, min(args.steps, 3))
@@ -330,6 +339,7 @@ def main():
                 t = float(tt.item())
             return out, t
 
+        _progress(rank, "optimiser leg")
         o = Options(max_evals=args.opt_evals)
         (hres, hrounds), t_host = timed(lambda: optimize_batch(batch, T, LBFGS(), o))
         (res, rounds), t_opt = timed(lambda: batch.optimize(T, LBFGS(), o, refit=True))
@@ -342,6 +352,7 @@ def main():
                "stopped_by": {k: sum(1 for r in res if r.stopped_by == k) for k in sorted({r.stopped_by for r in res})}}
     cpu = acc = None
     if rank == 0 and not args.no_cpu:
+        _progress(rank, "CPU baseline leg")
         if world == 1:  # the CPU baseline is an N=1 figure
             cpu, acc = cpu_baseline(X, Y, T, XT, gpu=r)
         else:  # N > 1: the metric's accuracy part only, on two of rank 0's slots
