@@ -8,15 +8,16 @@
 //     x3 = xk + v dt,  q3 = qk * wbar(w) * dt / 2,  wbar(w) = (sqrt(4/dt^2 - w.w), w)
 //     translational: g = C R(qa3)^T (xb3 + R(qb3) pb - xa3) - C pa
 //     rotational:    g = C Im(qa3^-1 * qb3)
-// One wave runs one trajectory's solve: lane i owns row i of F (n = 6 nb + nd <= 48 rows in LDS);
-// each sub-joint's rows and Jacobian blocks are built by one lane; the LU is LAPACK dgetf2's
+// One wave (projectv) or one workgroup (the rollout) runs one trajectory's solve with F in LDS
+// (n = 6 nb + nd <= 48 rows); each sub-joint's rows and Jacobian blocks are built by one lane of
+// wave 0; the LU is LAPACK dgetf2's
 // right-looking partial pivoting (first maximal |pivot|, reciprocal scaling, rank-1 update) and
 // dgetrs' unit-lower / upper substitutions, as Julia's F \ f.
 //
 // predictdynamics (examples/utils/predictdynamics.jl:7-22) for many trajectories: one 256-thread
 // workgroup per trajectory runs every step on the device -- the G GPs' mean predictions at the
-// current CState (the training points split over the workgroup), getvw, the projection (wave 0),
-// the projection error and updatestate!.
+// current CState (the training points split over the workgroup), getvw, the projection (its LU
+// update over the whole workgroup), the projection error and updatestate!.
 #include "gprx_internal.h"
 
 namespace gprx {
@@ -97,10 +98,21 @@ struct PState {
   double xk[PJ_MAXB][3], qk[PJ_MAXB][4];  // discrete pose (x2, q2)
   double xc[PJ_MAXB][3], qc[PJ_MAXB][4], vc[PJ_MAXB][3], wc[PJ_MAXB][3];
   double s[PJ_MAXN], su[6 * PJ_MAXB], f[PJ_MAXN], ds[PJ_MAXN];
-  double F[PJ_MAXN * (PJ_MAXN + 1)];     // row i at F[i * (n + 1)], n = 6 nb + nd
-  double A[PJ_MAXN * (PJ_MAXN + 1)];     // the LU's working copy of F
   int status, it;
 };
+// The Newton matrix F and the LU's working copy A live in dynamic LDS sized for the mechanism
+// (2 n (n + 1) doubles, n = 6 nb + nd; row i at i (n + 1)), so a small mechanism's workgroups are
+// not limited to the largest one's LDS footprint.
+__device__ __forceinline__ double* pj_lds() {
+  extern __shared__ __attribute__((aligned(16))) double pj_dyn[];
+  return pj_dyn;
+}
+#define PJ_F (pj_lds())
+#define PJ_A (pj_lds() + (size_t)(ldf - 1) * ldf)
+__host__ __device__ inline size_t pj_lds_bytes(int nb, int nd) {
+  const size_t n = 6 * (size_t)nb + nd;
+  return 2 * n * (n + 1) * sizeof(double);
+}
 __device__ __forceinline__ Qd ldq(const double* q) { return Qd{q[0], q[1], q[2], q[3]}; }
 
 // x3, q3 of body b (1-based; 0 = origin) at the current solution s
@@ -222,10 +234,10 @@ __device__ void subjoint(PState& P, const SubJoint& J, int n6, int ldf, double d
             tv += J.C[r][k] * (side ? Gv_a[k][j] : Gv_b[k][j]);
             tw += J.C[r][k] * (side ? Gw_a[k][j] : Gw_b[k][j]);
           }
-          P.F[row * ldf + c0 + j] = tv;
-          P.F[row * ldf + c0 + 3 + j] = tw;
-          P.F[(c0 + j) * ldf + row] = tv;
-          P.F[(c0 + 3 + j) * ldf + row] = tw;
+          PJ_F[row * ldf + c0 + j] = tv;
+          PJ_F[row * ldf + c0 + 3 + j] = tw;
+          PJ_F[(c0 + j) * ldf + row] = tv;
+          PJ_F[(c0 + 3 + j) * ldf + row] = tw;
         }
       }
     }
@@ -247,44 +259,62 @@ __device__ __forceinline__ double wsum(double v) {
 __device__ __forceinline__ void residual_upper(PState& P, int n6, int nd, int ldf, int l) {
   if (l < n6) {
     double t = 0.0;
-    for (int r = 0; r < nd; ++r) t += P.F[(n6 + r) * ldf + l] * P.s[n6 + r];
+    for (int r = 0; r < nd; ++r) t += PJ_F[(n6 + r) * ldf + l] * P.s[n6 + r];
     P.f[l] = (-P.su[l] + P.s[l]) + t;
   }
 }
 
-// projectv! on one wave (all 64 lanes call).  P.s holds the predicted (v, w) per body on entry
-// (lambda = 0 appended); leaves the projected (v, w) in P.s[0 .. 6nb).  P.xk / P.qk set.
-__device__ void project_wave(PState& P, const MechDev& M, double dt, double reg, double eps, int iters) {
-  const int l = threadIdx.x & 63;
+template <int NW>
+__device__ __forceinline__ void pj_sync() {
+  if constexpr (NW == 1) {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+  } else {
+    __syncthreads();
+  }
+}
+
+// projectv! on NW waves (all NW * 64 threads call).  P.s holds the predicted (v, w) per body on
+// entry (lambda = 0 appended); leaves the projected (v, w) in P.s[0 .. 6nb).  P.xk / P.qk set.
+// Wave 0 builds the constraints, Jacobians and residuals (one lane per sub-joint / row); the LU's
+// trailing update is spread over every thread, one element each; pivot search, the right-hand
+// side and the substitutions run redundantly on every wave (the same values), so no broadcast is
+// needed.  Each element sees the same operations in the same order for any NW.
+template <int NW>
+__device__ void project(PState& P, const MechDev& M, double dt, double reg, double eps, int iters) {
+  constexpr int NT = 64 * NW;
+  const int tid = threadIdx.x & (NT - 1), l = tid & 63;
+  const bool w0 = tid < 64;
   const int nb = M.nb, nd = M.nd, n6 = 6 * nb, n = n6 + nd, ldf = n + 1;
-  for (int i = l; i < n * ldf; i += 64) P.F[i] = 0.0;
-  __builtin_amdgcn_wave_barrier();
-  if (l < n6) P.su[l] = P.s[l];
-  if (l >= n6 && l < n) P.s[l] = 0.0;
-  __builtin_amdgcn_wave_barrier();
-  if (l < M.nsub) subjoint(P, M.sub[l], n6, ldf, dt, false, true);  // updateF!
-  __builtin_amdgcn_wave_barrier();
-  if (l < n) P.F[l * ldf + l] = (l < n6 ? 1.0 : 0.0) + reg;        // F += I * regularizer
-  if (l == 0) {
+  for (int i = tid; i < n * ldf; i += NT) PJ_F[i] = 0.0;
+  pj_sync<NW>();
+  if (w0) {
+    if (l < n6) P.su[l] = P.s[l];
+    if (l >= n6 && l < n) P.s[l] = 0.0;
+  }
+  pj_sync<NW>();
+  if (w0 && l < M.nsub) subjoint(P, M.sub[l], n6, ldf, dt, false, true);  // updateF!
+  pj_sync<NW>();
+  if (w0 && l < n) PJ_F[l * ldf + l] = (l < n6 ? 1.0 : 0.0) + reg;        // F += I * regularizer
+  if (tid == 0) {
     P.status = 0;
     P.it = 0;
   }
-  __builtin_amdgcn_wave_barrier();
+  pj_sync<NW>();
   for (int it = 1; it <= iters; ++it) {
-    if (l < M.nsub) subjoint(P, M.sub[l], n6, ldf, dt, true, true);  // updateF! + g(mechanism)
-    __builtin_amdgcn_wave_barrier();
-    residual_upper(P, n6, nd, ldf, l);
-    __builtin_amdgcn_wave_barrier();
+    if (w0 && l < M.nsub) subjoint(P, M.sub[l], n6, ldf, dt, true, true);  // updateF! + g(mechanism)
+    pj_sync<NW>();
+    if (w0) residual_upper(P, n6, nd, ldf, l);
+    pj_sync<NW>();
     // ---- ds = F \ f: LU with partial pivoting of a working copy A (F keeps the Newton matrix;
     // its G blocks are rebuilt by the next updateF!)
-    if (l < n)
-      for (int j = 0; j < n; ++j) P.A[l * ldf + j] = P.F[l * ldf + j];
+    for (int i = tid; i < n * ldf; i += NT) PJ_A[i] = PJ_F[i];
     double b = l < n ? P.f[l] : 0.0;
-    __builtin_amdgcn_wave_barrier();
+    pj_sync<NW>();
     bool singular = false;
     for (int k = 0; k < n; ++k) {
       // pivot: first row of maximal |a_ik|, i >= k (idamax)
-      double v = (l >= k && l < n) ? fabs(P.A[l * ldf + k]) : -1.0;
+      double v = (l >= k && l < n) ? fabs(PJ_A[l * ldf + k]) : -1.0;
       int idx = l;
       for (int o = 1; o < 64; o <<= 1) {
         const double v2 = __shfl_xor(v, o);
@@ -296,59 +326,74 @@ __device__ void project_wave(PState& P, const MechDev& M, double dt, double reg,
       }
       const int p = idx;
       if (p != k) {  // swap rows k and p of A and of the right-hand side
-        for (int j = l; j < n; j += 64) {
-          const double t = P.A[k * ldf + j];
-          P.A[k * ldf + j] = P.A[p * ldf + j];
-          P.A[p * ldf + j] = t;
+        if (NW > 1) pj_sync<NW>();  // every wave has read column k
+        for (int j = tid; j < n; j += NT) {
+          const double t = PJ_A[k * ldf + j];
+          PJ_A[k * ldf + j] = PJ_A[p * ldf + j];
+          PJ_A[p * ldf + j] = t;
         }
         const double bk = readlane_dbl(b, k), bp = readlane_dbl(b, p);
         if (l == k) b = bp;
         if (l == p) b = bk;
       }
-      __builtin_amdgcn_wave_barrier();
-      const double akk = P.A[k * ldf + k];
+      pj_sync<NW>();
+      const double akk = PJ_A[k * ldf + k];
       if (akk == 0.0) singular = true;
-      if (l > k && l < n && akk != 0.0) {
-        const double lk = fabs(akk) >= DBL_MIN ? P.A[l * ldf + k] * (1.0 / akk) : P.A[l * ldf + k] / akk;
-        P.A[l * ldf + k] = lk;
-        for (int j = k + 1; j < n; ++j) P.A[l * ldf + j] = P.A[l * ldf + j] - lk * P.A[k * ldf + j];
+      const int m = n - 1 - k;
+      if (akk != 0.0 && m > 0) {
+        if (w0 && l > k && l < n)
+          PJ_A[l * ldf + k] = fabs(akk) >= DBL_MIN ? PJ_A[l * ldf + k] * (1.0 / akk) : PJ_A[l * ldf + k] / akk;
+        pj_sync<NW>();
+        // trailing update A[i][j] -= l_i A[k][j], i, j in (k, n): element e = (i - k - 1) m + (j - k - 1)
+        const int si = NT / m, sj = NT - si * m;
+        int i = tid / m, j = tid - i * m;
+        for (int e = tid; e < m * m; e += NT) {
+          const int gi = k + 1 + i, gj = k + 1 + j;
+          PJ_A[gi * ldf + gj] = PJ_A[gi * ldf + gj] - PJ_A[gi * ldf + k] * PJ_A[k * ldf + gj];
+          i += si;
+          j += sj;
+          if (j >= m) {
+            j -= m;
+            ++i;
+          }
+        }
       }
-      __builtin_amdgcn_wave_barrier();
+      pj_sync<NW>();
     }
     if (singular) {  // Julia's F \ f throws SingularException: the trajectory stops
-      if (l == 0) P.status = 1;
-      __builtin_amdgcn_wave_barrier();
+      if (tid == 0) P.status = 1;
+      pj_sync<NW>();
       return;
     }
     // forward substitution (unit lower), then backward (upper), as dgetrs / dtrsm
     for (int k = 0; k < n; ++k) {
       const double bk = readlane_dbl(b, k);
-      if (bk != 0.0 && l > k && l < n) b = b - bk * P.A[l * ldf + k];
+      if (bk != 0.0 && l > k && l < n) b = b - bk * PJ_A[l * ldf + k];
     }
     for (int k = n - 1; k >= 0; --k) {
-      const double ukk = P.A[k * ldf + k];
+      const double ukk = PJ_A[k * ldf + k];
       double bk = readlane_dbl(b, k);
       if (bk != 0.0) {
         bk = bk / ukk;
         if (l == k) b = bk;
-        if (l < k) b = b - bk * P.A[l * ldf + k];
+        if (l < k) b = b - bk * PJ_A[l * ldf + k];
       }
     }
     // s -= ds, updateMechanism!
-    if (l < n) {
+    if (w0 && l < n) {
       P.ds[l] = b;
       P.s[l] = P.s[l] - b;
     }
-    __builtin_amdgcn_wave_barrier();
+    pj_sync<NW>();
     // convergence: |f(s_new)| (with the iteration's G) and |ds|
-    if (l < M.nsub) subjoint(P, M.sub[l], n6, ldf, dt, true, false);
-    __builtin_amdgcn_wave_barrier();
-    residual_upper(P, n6, nd, ldf, l);
-    __builtin_amdgcn_wave_barrier();
+    if (w0 && l < M.nsub) subjoint(P, M.sub[l], n6, ldf, dt, true, false);
+    pj_sync<NW>();
+    if (w0) residual_upper(P, n6, nd, ldf, l);
+    pj_sync<NW>();
     const double fv = l < n ? P.f[l] : 0.0, dv = l < n ? P.ds[l] : 0.0;
     const double nf = sqrt(wsum(fv * fv)), nds = sqrt(wsum(dv * dv));
-    if (l == 0) P.it = it;
-    __builtin_amdgcn_wave_barrier();
+    if (tid == 0) P.it = it;
+    pj_sync<NW>();
     if (nf < eps && nds < eps) break;
   }
 }
@@ -401,14 +446,14 @@ __device__ __forceinline__ double cstate_at(const PState& P, int i) {
 }  // namespace
 
 // ---- projectv! for T independent mechanism states: one wave each ------------------------------
-__global__ __launch_bounds__(64) void k_project(ProjArgs a) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_project(ProjArgs a) {
   __shared__ PState P;
   const int t = blockIdx.x, l = threadIdx.x;
   const int nb = a.mech.nb, n6 = 6 * nb;
   set_states(P, a.cs + (size_t)t * 13 * nb, nb, a.dt, l);
   if (l < n6) P.s[l] = a.vw[(size_t)t * n6 + l];
   __builtin_amdgcn_wave_barrier();
-  project_wave(P, a.mech, a.dt, a.reg, a.eps, a.iters);
+  project<1>(P, a.mech, a.dt, a.reg, a.eps, a.iters);
   __builtin_amdgcn_wave_barrier();
   if (l < n6) a.out[(size_t)t * n6 + l] = P.status ? NAN : P.s[l];
   if (l == 0) {
@@ -419,7 +464,7 @@ __global__ __launch_bounds__(64) void k_project(ProjArgs a) {
 
 // ---- predictdynamics: one workgroup per trajectory, every step on the device --------------------
 template <int MODE>
-__global__ __launch_bounds__(256) void k_rollout_max(RolloutMaxArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_rollout_max(RolloutMaxArgs a) {
   constexpr int NT = 256, NW = NT / 64;
   __shared__ PState P;
   __shared__ double obs[13 * PJ_MAXB];
@@ -471,9 +516,10 @@ __global__ __launch_bounds__(256) void k_rollout_max(RolloutMaxArgs a) {
         const int pos = a.vw[l], b = pos / 13, k = pos - 13 * b;  // k in 7..12
         P.s[6 * b + (k - 7)] = mu;
       }
-      __builtin_amdgcn_wave_barrier();
-      project_wave(P, a.mech, a.dt, a.reg, a.eps, a.iters);
-      __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+    project<NW>(P, a.mech, a.dt, a.reg, a.eps, a.iters);  // the whole workgroup
+    if (w == 0) {
       // projection error |(v, w)_const - (v, w)_pred| (predictdynamics.jl:16), then updatestate!
       const double dv = l < n6 ? P.s[l] - P.su[l] : 0.0;
       const double e = sqrt(wsum(dv * dv));
@@ -496,12 +542,13 @@ __global__ __launch_bounds__(256) void k_rollout_max(RolloutMaxArgs a) {
 }
 
 void launch_project(const ProjArgs& a, hipStream_t s) {
-  if (a.T > 0) hipLaunchKernelGGL(k_project, dim3(a.T), dim3(64), 0, s, a);
+  if (a.T > 0) hipLaunchKernelGGL(k_project, dim3(a.T), dim3(64), pj_lds_bytes(a.mech.nb, a.mech.nd), s, a);
 }
 void launch_rollout_max(const RolloutMaxArgs& a, int dist_mode, hipStream_t s) {
   if (a.T <= 0) return;
-  if (dist_mode == 0) hipLaunchKernelGGL(k_rollout_max<0>, dim3(a.T), dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(k_rollout_max<1>, dim3(a.T), dim3(256), 0, s, a);
+  const size_t lds = pj_lds_bytes(a.mech.nb, a.mech.nd);
+  if (dist_mode == 0) hipLaunchKernelGGL(k_rollout_max<0>, dim3(a.T), dim3(256), lds, s, a);
+  else hipLaunchKernelGGL(k_rollout_max<1>, dim3(a.T), dim3(256), lds, s, a);
 }
 
 }  // namespace gprx
