@@ -69,6 +69,14 @@ struct LbView {
   double *x, *g, *s, *gp, *xr, *xp, *dx, *cx, *cg, *th0, *dxh, *dgh, *rho, *al, *sc;
   int* iv;
 };
+__device__ __forceinline__ LbView lb_view_at(int n, int m, double* w, int* iv) {
+  LbView v;
+  v.x = w; v.g = w + n; v.s = w + 2 * n; v.gp = w + 3 * n; v.xr = w + 4 * n; v.xp = w + 5 * n;
+  v.dx = w + 6 * n; v.cx = w + 7 * n; v.cg = w + 8 * n; v.th0 = w + 9 * n;
+  v.dxh = w + 10 * n; v.dgh = v.dxh + m * n; v.rho = v.dgh + m * n; v.al = v.rho + m; v.sc = v.al + m;
+  v.iv = iv;
+  return v;
+}
 __device__ __forceinline__ LbView lb_view(const LbArgs& a, int slot) {
   const int n = a.n, m = a.m;
   double* w = a.ws + (size_t)slot * lb_ws_doubles(n, m);
@@ -123,11 +131,9 @@ __device__ void lb_write_params(const LbArgs& a, const DevBatch& db, int slot, c
   derive_params(db, slot);
 }
 
-__global__ __launch_bounds__(64) void k_lbfgs(LbArgs a, DevBatch db, int init) {
-  const int slot = blockIdx.x * 64 + threadIdx.x;
-  if (slot >= db.B) return;
+// One slot's optimiser between two evaluations (one thread; v: its state, in LDS or in HBM)
+__device__ void lbfgs_slot(const LbArgs& a, const DevBatch& db, int slot, int init, const LbView& v) {
   const int n = a.n, m = a.m;
-  LbView v = lb_view(a, slot);
   int* I = v.iv;
   double* S = v.sc;
   if (init) {
@@ -351,6 +357,31 @@ __global__ __launch_bounds__(64) void k_lbfgs(LbArgs a, DevBatch db, int init) {
   ri[3] = I[I_STOP] | (I[I_CONV] ? 0x100 : 0);
 }
 
+// One workgroup per slot: the slot's state (a few KB) is copied into LDS by the whole wave, the
+// state machine runs on lane 0 against LDS (its dependent loads no longer wait on L2), and the
+// state is written back.  The arithmetic is lbfgs_slot's either way.  States too large for LDS
+// (m and d at the ABI's limits) run in place in HBM.
+__global__ __launch_bounds__(64) void k_lbfgs(LbArgs a, DevBatch db, int init) {
+  extern __shared__ __attribute__((aligned(16))) double lws[];
+  const int slot = blockIdx.x, l = threadIdx.x;
+  if (slot >= db.B) return;
+  const size_t nws = lb_ws_doubles(a.n, a.m);
+  if (!a.lds) {
+    if (l == 0) lbfgs_slot(a, db, slot, init, lb_view(a, slot));
+    return;
+  }
+  double* gw = a.ws + (size_t)slot * nws;
+  int* gi = a.iws + (size_t)slot * LB_NI;
+  int* liv = (int*)(lws + nws);
+  for (size_t i = l; i < nws; i += 64) lws[i] = gw[i];
+  if (l < LB_NI) liv[l] = gi[l];
+  __syncthreads();
+  if (l == 0) lbfgs_slot(a, db, slot, init, lb_view_at(a.n, a.m, lws, liv));
+  __syncthreads();
+  for (size_t i = l; i < nws; i += 64) gw[i] = lws[i];
+  if (l < LB_NI) gi[l] = liv[l];
+}
+
 // the minimiser's kernel parameters (Optim's result -> set_params!; update_target! follows).  The
 // minimiser is written as it is: a non-finite one (the NaN-gradient stop of a non-PD start) makes
 // derive_params mark the slot GPRX_INVALID_ARGUMENT, so the refit reports it instead of quietly
@@ -364,8 +395,14 @@ __global__ __launch_bounds__(64) void k_lbfgs_final(LbArgs a, DevBatch db) {
   derive_params(db, slot);
 }
 
+size_t lbfgs_lds_bytes(int n, int m) { return lb_ws_doubles(n, m) * sizeof(double) + LB_NI * sizeof(int); }
 void launch_lbfgs(const LbArgs& a, const DevBatch& db, int init, hipStream_t s) {
-  hipLaunchKernelGGL(k_lbfgs, dim3((db.B + 63) / 64), dim3(64), 0, s, a, db, init);
+  static bool attr = false;
+  if (!attr) {  // up to the CU's 160 KB (the default cap is 64 KB)
+    (void)hipFuncSetAttribute((const void*)k_lbfgs, hipFuncAttributeMaxDynamicSharedMemorySize, LB_LDS_MAX);
+    attr = true;
+  }
+  hipLaunchKernelGGL(k_lbfgs, dim3(db.B), dim3(64), a.lds ? lbfgs_lds_bytes(a.n, a.m) : 0, s, a, db, init);
 }
 void launch_lbfgs_final(const LbArgs& a, const DevBatch& db, hipStream_t s) {
   hipLaunchKernelGGL(k_lbfgs_final, dim3((db.B + 63) / 64), dim3(64), 0, s, a, db);

@@ -1,6 +1,6 @@
 """k_rollout_max / k_project timing for FB (the sweep's slowest groups): T trajectories of `steps`
 steps, and T single projections."""
-import sys, time
+import sys, time, hashlib
 sys.path[:0] = ['/root/repo', '/root/repo/gpr.jl_amd']
 import numpy as np, gprx
 import gprx.data as D
@@ -20,7 +20,8 @@ for mech in sys.argv[1:] or ['FB']:
         t0 = time.perf_counter()
         out, pe, st = GP.predictdynamics(mech, [[(b, g) for g in range(G)]], S, steps, idx)
         dt = time.perf_counter() - t0
-        print(mech, 'rollout_max T', T, 'steps', steps, f'{dt*1e3:.1f} ms', 'ok', int((st == 0).sum()), flush=True)
+        print(mech, 'rollout_max T', T, 'steps', steps, f'{dt*1e3:.1f} ms', 'ok', int((st == 0).sum()),
+              'digest', hashlib.md5(out.tobytes()).hexdigest()[:8], hashlib.md5(pe.tobytes()).hexdigest()[:8], flush=True)
     nb = GP.NBODIES[mech]
     X = D._cstates(mech, D._sample_minimal(mech, T, np.random.default_rng(1))).T
     rng = np.random.default_rng(2)
@@ -29,5 +30,6 @@ for mech in sys.argv[1:] or ['FB']:
     t0 = time.perf_counter()
     out, it, st = GP.projectv(mech, X, vw)
     dt = time.perf_counter() - t0
-    print(mech, 'projectv T', T, f'{dt*1e3:.1f} ms', 'mean iters', float(it.mean()), 'ok', int((st == 0).sum()), flush=True)
+    print(mech, 'projectv T', T, f'{dt*1e3:.1f} ms', 'mean iters', float(it.mean()), 'ok', int((st == 0).sum()),
+          'digest', hashlib.md5(out.tobytes()).hexdigest()[:8], hashlib.md5(it.tobytes()).hexdigest()[:8], flush=True)
     b.close()
