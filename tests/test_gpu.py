@@ -536,6 +536,34 @@ def test_device_optimize_matches_host_lockstep(gprx, ctx, golden_dir, name, max_
     assert dr == hr
 
 
+def test_device_optimize_ragged_batch_equals_single_slot_runs(gprx, ctx, golden_dir):
+    """Slots that stop at different rounds (Optim's own stops, no budget): finished slots are
+    masked out of the later rounds' evaluations, and every slot's result is bit-identical to
+    optimising that GP alone."""
+    from gprx.optim import LBFGS, Options
+
+    z = np.load(golden_dir / "p2_n100.npz")
+    X, Y, th = z["X"], z["Y"], z["theta"]
+    B = Y.shape[0]
+    rng = np.random.default_rng(11)
+    th0 = np.stack([th + 0.2 * rng.standard_normal(th.shape[0]) for _ in range(B)])
+    opts = Options(iterations=60)
+    b = gprx.GPBatch(B, X.shape[0], X.shape[1], 0, ctx=ctx)
+    b.set_train(X, Y)
+    dev, rounds = b.optimize(th0, LBFGS(), opts, refit=False)
+    assert len({r.f_calls for r in dev}) > 1  # ragged: the slots stop at different rounds
+    one = gprx.GPBatch(1, X.shape[0], X.shape[1], 0, ctx=ctx)
+    for s in range(B):
+        one.set_train(X, Y[s:s + 1])
+        (r1,), _ = one.optimize(th0[s:s + 1], LBFGS(), opts, refit=False)
+        assert (r1.iterations, r1.f_calls, r1.g_calls, r1.stopped_by) == (
+            dev[s].iterations, dev[s].f_calls, dev[s].g_calls, dev[s].stopped_by), s
+        np.testing.assert_array_equal(r1.minimizer, dev[s].minimizer)
+        assert r1.minimum == dev[s].minimum
+    one.close()
+    b.close()
+
+
 def test_device_optimize_to_convergence_and_refit(gprx, ctx, golden_dir):
     """optimize! to Optim's own stop (no budget) on every slot, then update_target!: the batch is
     left factorised at the minimisers, so predict() answers for them."""
