@@ -162,7 +162,8 @@ void gprx_opt_defaults(gprx_opt_options* opt);
 /* theta0[B*(d+2)] start points; outputs (host, any may be NULL): theta_out[B*(d+2)] minimisers,
  * minimum[B] = -mll at the minimiser as Optim reports it, iterations/f_calls/g_calls[B],
  * stopped[B] = GPRX_STOP_* | GPRX_STOP_CONVERGED, rounds = batch evaluations performed
- * (excluding the refit).  Returns GPRX_OK, or an error of the evaluations themselves
+ * (excluding the refit; a round evaluates only the slots whose optimisers are still running, so a
+ * ragged batch costs less per round as slots finish).  Returns GPRX_OK, or an error of the evaluations themselves
  * (device / memory); per-slot failures during the search are +Inf answers, not errors.  With
  * refit, a minimiser whose refit fails (not finite: GPRX_INVALID_ARGUMENT; not positive definite:
  * GPRX_NOT_POSITIVE_DEFINITE) is returned as that status (first failing slot), the outputs are
