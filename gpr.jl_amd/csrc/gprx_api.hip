@@ -736,7 +736,6 @@ int gprx_batch_optimize(gprx_batch* b, const double* theta0, const gprx_opt_opti
   a.c_1 = o.c_1;
   a.rho_hi = o.rho_hi;
   a.rho_lo = o.rho_lo;
-  a.lds = gprx::lbfgs_lds_bytes(n, o.m) <= (size_t)gprx::LB_LDS_MAX ? 1 : 0;
   // one device block: state, start points, flags, results; one pinned host mirror of the flags
   // and results
   const size_t wsd = (size_t)B * gprx::lb_ws_doubles(n, o.m), rd = (size_t)B * (n + 1);

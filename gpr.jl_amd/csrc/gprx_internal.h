@@ -196,7 +196,6 @@ struct LbArgs {
   double* result;        // B x (n + 1): x, f(x) = -mll
   int* result_i;         // B x 4: iterations, f calls, g calls, stop | converged
   int n, m, max_evals, iterations, ls_iterations, scaleinvH0, successive_f_tol, time_up;
-  int lds;               // 1: each slot's state runs from LDS (lbfgs_lds_bytes(n, m) <= LB_LDS_MAX)
   double g_abstol, alphaguess, c_1, rho_hi, rho_lo;
 };
 constexpr int LB_LDS_MAX = 160 * 1024;

@@ -357,19 +357,16 @@ __device__ void lbfgs_slot(const LbArgs& a, const DevBatch& db, int slot, int in
   ri[3] = I[I_STOP] | (I[I_CONV] ? 0x100 : 0);
 }
 
-// One workgroup per slot: the slot's state (a few KB) is copied into LDS by the whole wave, the
-// state machine runs on lane 0 against LDS (its dependent loads no longer wait on L2), and the
-// state is written back.  The arithmetic is lbfgs_slot's either way.  States too large for LDS
-// (m and d at the ABI's limits) run in place in HBM.
+// One workgroup per slot: the slot's state (at most 74 KB: m = 64, d = DMAX) is copied into LDS
+// by the whole wave, the state machine runs on lane 0 against LDS (its dependent loads no longer
+// wait on L2), and the state is written back.
+static_assert((size_t)(10 + 2 * 64) * (DMAX + 2) * 8 + (2 * 64 + LB_NS) * 8 + LB_NI * 4 <= (size_t)LB_LDS_MAX,
+              "the largest optimiser state fits in LDS");
 __global__ __launch_bounds__(64) void k_lbfgs(LbArgs a, DevBatch db, int init) {
   extern __shared__ __attribute__((aligned(16))) double lws[];
   const int slot = blockIdx.x, l = threadIdx.x;
   if (slot >= db.B) return;
   const size_t nws = lb_ws_doubles(a.n, a.m);
-  if (!a.lds) {
-    if (l == 0) lbfgs_slot(a, db, slot, init, lb_view(a, slot));
-    return;
-  }
   double* gw = a.ws + (size_t)slot * nws;
   int* gi = a.iws + (size_t)slot * LB_NI;
   int* liv = (int*)(lws + nws);
@@ -402,7 +399,7 @@ void launch_lbfgs(const LbArgs& a, const DevBatch& db, int init, hipStream_t s) 
     (void)hipFuncSetAttribute((const void*)k_lbfgs, hipFuncAttributeMaxDynamicSharedMemorySize, LB_LDS_MAX);
     attr = true;
   }
-  hipLaunchKernelGGL(k_lbfgs, dim3(db.B), dim3(64), a.lds ? lbfgs_lds_bytes(a.n, a.m) : 0, s, a, db, init);
+  hipLaunchKernelGGL(k_lbfgs, dim3(db.B), dim3(64), lbfgs_lds_bytes(a.n, a.m), s, a, db, init);
 }
 void launch_lbfgs_final(const LbArgs& a, const DevBatch& db, hipStream_t s) {
   hipLaunchKernelGGL(k_lbfgs_final, dim3((db.B + 63) / 64), dim3(64), 0, s, a, db);
