@@ -152,65 +152,90 @@ def _oracle_fit_worker(args):
 
 
 def cpu_baseline(X, Y, T, XT, gpu=None, max_seconds: float = 15.0, max_fits: int = 32, modes=("single", "parallel")):
-    """The oracle (CPU restatement of the reference algorithm: numpy + host OpenBLAS LAPACK) timed
-    on a bounded sample of the same workload, in the two SURVEY.md section 8d modes:
+    """The CPU restatement of the reference algorithm timed on a bounded sample of the same
+    workload, in the two SURVEY.md section 8d modes:
       single   one fit at a time, BLAS on every used core;
-      parallel trial-parallel: one fit per process, BLAS single-threaded, one process per used
-               core (the reference's Threads.@threads over trials, core.jl:28).
-    With `gpu` (the last timed step's results) the single-mode sample also gives the metric's
-    accuracy part: max |mu_gpu - mu_cpu| of the predictive means (BASELINE.json 'pred-mean
-    max-err').  Returns (baseline dict, accuracy dict)."""
+      parallel trial-parallel: whole fits on every used core at once, BLAS single-threaded (the
+               reference's Threads.@threads over trials, core.jl:28).
+    Timed implementation: oracle/cpu_fit.c (C on the host's OpenBLAS, OpenMP threads for the
+    trial-parallel mode), or the numpy oracle when libcpufit.so is absent.
+    With `gpu` (the last timed step's results) a few slots are also checked against the numpy oracle
+    (oracle/gp_oracle.py): the metric's accuracy part, max |mu_gpu - mu_cpu| of the predictive
+    means (BASELINE.json 'pred-mean max-err').  Returns (baseline dict, accuracy dict)."""
     sys.path.insert(0, str(REPO))
     from oracle import gp_oracle as O
     from threadpoolctl import threadpool_limits
 
     cores, nproc = _host_cores()
     out = {}
+    impl = "numpy"
+    try:
+        from oracle import cpu_fit as CF
+
+        CF.load()
+        impl = "c"
+    except OSError:
+        CF = None
+    if impl == "c":
+        if "single" in modes:
+            n, dt = CF.timed(X, Y, T, XT, threads=1, blas_threads=cores, max_seconds=max_seconds, max_fits=max_fits)
+            out["single"] = dict(value=n / dt, fits=n, seconds=round(dt, 2), blas_threads=cores)
+        if "parallel" in modes:
+            n, dt = CF.timed(X, Y, T, XT, threads=cores, blas_threads=1, max_seconds=max_seconds,
+                             max_fits=max(max_fits, 16 * cores))
+            out["parallel"] = dict(value=n / dt, fits=n, seconds=round(dt, 2), threads=cores, blas_threads_each=1)
+    else:
+        if "single" in modes:
+            t0 = time.perf_counter()
+            n = 0
+            with threadpool_limits(cores):
+                for s in range(min(max_fits, X.shape[0])):
+                    O.fit(X[s], Y[s], T[s], XT[s])
+                    n += 1
+                    if time.perf_counter() - t0 > max_seconds:
+                        break
+            dt = time.perf_counter() - t0
+            out["single"] = dict(value=n / dt, fits=n, seconds=round(dt, 2), blas_threads=cores)
+        if "parallel" in modes:
+            import multiprocessing as mp
+
+            P = cores
+            deadline = time.time() + max_seconds
+            # every process gets its own slots (round robin), enough for the deadline
+            per = max(2, max_fits // P + 2)
+            jobs = [([(k + P * i) % X.shape[0] for i in range(per)], X, Y, T, XT, deadline) for k in range(P)]
+            t0 = time.perf_counter()
+            with mp.get_context("fork").Pool(P) as pool:
+                counts = pool.map(_oracle_fit_worker, jobs)
+            dt = time.perf_counter() - t0
+            out["parallel"] = dict(value=sum(counts) / dt, fits=int(sum(counts)), seconds=round(dt, 2), processes=P,
+                                   blas_threads_each=1)
     err = dict(mu_abs=0.0, mu_rel=0.0, mll_rel=0.0, grad_rel=0.0)
     n_err = 0
-    if "single" in modes:
-        t0 = time.perf_counter()
-        n = 0
+    if gpu is not None:  # accuracy on a few slots against the numpy oracle
         with threadpool_limits(cores):
-            for s in range(min(max_fits, X.shape[0])):
+            for s in range(min(4, X.shape[0])):
                 f = O.fit(X[s], Y[s], T[s], XT[s])
-                n += 1
-                if gpu is not None:
-                    e_mu = float(np.max(np.abs(gpu["mu"][s] - f["mu"])))
-                    err["mu_abs"] = max(err["mu_abs"], e_mu)
-                    err["mu_rel"] = max(err["mu_rel"], e_mu / float(np.max(np.abs(Y[s]))))
-                    err["mll_rel"] = max(err["mll_rel"], abs(gpu["mll"][s] - f["mll"]) / max(1.0, abs(f["mll"])))
-                    err["grad_rel"] = max(err["grad_rel"], float(np.max(np.abs(gpu["grad"][s] - f["grad"])))
-                                          / max(1.0, float(np.max(np.abs(f["grad"])))))
-                    n_err += 1
-                if time.perf_counter() - t0 > max_seconds:
-                    break
-        dt = time.perf_counter() - t0
-        out["single"] = dict(value=n / dt, fits=n, seconds=round(dt, 2), blas_threads=cores)
-    if "parallel" in modes:
-        import multiprocessing as mp
-
-        P = cores
-        deadline = time.time() + max_seconds
-        # every process gets its own slots (round robin), enough for the deadline
-        per = max(2, max_fits // P + 2)
-        jobs = [([(k + P * i) % X.shape[0] for i in range(per)], X, Y, T, XT, deadline) for k in range(P)]
-        t0 = time.perf_counter()
-        with mp.get_context("fork").Pool(P) as pool:
-            counts = pool.map(_oracle_fit_worker, jobs)
-        dt = time.perf_counter() - t0
-        out["parallel"] = dict(value=sum(counts) / dt, fits=int(sum(counts)), seconds=round(dt, 2), processes=P,
-                               blas_threads_each=1)
+                e_mu = float(np.max(np.abs(gpu["mu"][s] - f["mu"])))
+                err["mu_abs"] = max(err["mu_abs"], e_mu)
+                err["mu_rel"] = max(err["mu_rel"], e_mu / float(np.max(np.abs(Y[s]))))
+                err["mll_rel"] = max(err["mll_rel"], abs(gpu["mll"][s] - f["mll"]) / max(1.0, abs(f["mll"])))
+                err["grad_rel"] = max(err["grad_rel"], float(np.max(np.abs(gpu["grad"][s] - f["grad"])))
+                                      / max(1.0, float(np.max(np.abs(f["grad"])))))
+                n_err += 1
     best = max(out, key=lambda k: out[k]["value"])
+    how = ("oracle/cpu_fit.c: C on the host's OpenBLAS (dpotrf/dpotrs/dtrsm), OpenMP threads for the trial-parallel "
+           "mode" if impl == "c" else "oracle/gp_oracle.py: numpy + the host's OpenBLAS")
     base = dict(value=out[best]["value"], unit="fits/s", cores=cores, kind="port", nproc=nproc, mode=best, modes=out,
-                sample=f"P2 fits (N=2048, d=26, M=100) of the bench workload via oracle/gp_oracle.py (reference "
-                       f"algorithm: distij direct distances, OpenBLAS dpotrf, K^-1 by cho_solve(I), per-parameter "
+                impl=impl,
+                sample=f"P2 fits (N=2048, d=26, M=100) of the bench workload via {how} (reference algorithm: "
+                       f"KernelData distance stack, direct distances, dpotrf, K^-1 by dpotrs on I, per-parameter "
                        f"gradient sums), each mode bounded to ~{max_seconds:.0f} s; value = the faster mode ({best}); "
                        f"{cores} of nproc={nproc} host CPUs used")
     acc = None
     if gpu is not None and n_err:
         acc = dict(err, slots=n_err, tolerance_mu_rel=1e-9, tolerance_mll_rel=1e-10, tolerance_grad_rel=1e-7,
-                   note="GPU vs CPU restatement on the same inputs; mu_rel = max|dmu| / max|y|")
+                   note="GPU vs CPU restatement (oracle/gp_oracle.py) on the same inputs; mu_rel = max|dmu| / max|y|")
     return base, acc
 
 
