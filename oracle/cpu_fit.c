@@ -28,11 +28,13 @@ typedef void (*potrs_t)(const char*, const int*, const int*, const double*, cons
 typedef void (*trsm_t)(const char*, const char*, const char*, const char*, const int*, const int*, const double*,
                        const double*, const int*, double*, const int*, size_t, size_t, size_t, size_t);
 typedef void (*nthreads_t)(int);
+typedef int (*getthreads_t)(void);
 
 static potrf_t dpotrf_;
 static potrs_t dpotrs_;
 static trsm_t dtrsm_;
 static nthreads_t set_threads_;
+static getthreads_t get_threads_;
 
 #define LOG2PI 1.8378770664093453
 #define EPS 2.220446049250313e-16
@@ -45,29 +47,58 @@ int cpufit_init(const char* openblas_path) {
   dpotrs_ = (potrs_t)dlsym(h, "scipy_dpotrs_");
   dtrsm_ = (trsm_t)dlsym(h, "scipy_dtrsm_");
   set_threads_ = (nthreads_t)dlsym(h, "scipy_openblas_set_num_threads");
-  return (dpotrf_ && dpotrs_ && dtrsm_ && set_threads_) ? 0 : 2;
+  get_threads_ = (getthreads_t)dlsym(h, "scipy_openblas_get_num_threads");
+  return (dpotrf_ && dpotrs_ && dtrsm_ && set_threads_ && get_threads_) ? 0 : 2;
 }
 
+/* The library is the one scipy itself loaded: every call that changes its thread count restores
+ * it, so numpy/scipy results elsewhere in the process are not perturbed. */
 void cpufit_blas_threads(int n) { set_threads_(n); }
+int cpufit_get_blas_threads(void) { return get_threads_(); }
+
+/* per-fit workspace: the distance stack and four N x N matrices, reused across fits */
+typedef struct {
+  size_t cap;
+  double* buf;
+} Work;
+static double* work_get(Work* w, size_t need) {
+  if (need > w->cap) {
+    free(w->buf);
+    w->buf = malloc(sizeof(double) * need);
+    w->cap = w->buf ? need : 0;
+  }
+  return w->buf;
+}
+static size_t work_need(int d, int N, int M) {
+  const size_t NN = (size_t)N * N;
+  return (size_t)d * NN + 3 * NN + (size_t)N + (size_t)d + (size_t)N * M;
+}
+static int fit_ws(int d, int N, int M, const double* X, const double* y, const double* theta, const double* Xs,
+                  double* mll, double* grad, double* mu, double* var, double* ws);
 
 /* One fit.  X: d x N (x_p of point j at X[p N + j]), y: N, theta: d + 2 ([log sn, log ell_1..d,
  * log sf]), Xs: d x M (may be NULL when M = 0).  Outputs: *mll, grad[d+2], mu[M], var[M].
  * Returns 0, or the dpotrf info (> 0: not positive definite), or -1 (allocation). */
 int cpufit_fit(int d, int N, int M, const double* X, const double* y, const double* theta, const double* Xs,
                double* mll, double* grad, double* mu, double* var) {
+  Work w = {0, NULL};
+  double* ws = work_get(&w, work_need(d, N, M));
+  const int rc = ws ? fit_ws(d, N, M, X, y, theta, Xs, mll, grad, mu, var, ws) : -1;
+  free(w.buf);
+  return rc;
+}
+
+static int fit_ws(int d, int N, int M, const double* X, const double* y, const double* theta, const double* Xs,
+                  double* mll, double* grad, double* mu, double* var, double* ws) {
   const size_t NN = (size_t)N * N;
-  double* D = malloc(sizeof(double) * (size_t)d * NN);
-  double* Kf = malloc(sizeof(double) * NN);
-  double* K = malloc(sizeof(double) * NN);
-  double* Ki = malloc(sizeof(double) * NN);
-  double* al = malloc(sizeof(double) * N);
-  double* il2 = malloc(sizeof(double) * d);
-  double* Ks = M > 0 ? malloc(sizeof(double) * (size_t)N * M) : NULL;
+  double* D = ws;
+  double* Kf = D + (size_t)d * NN;
+  double* K = Kf + NN;
+  double* Ki = K + NN;
+  double* al = Ki + NN;
+  double* il2 = al + N;
+  double* Ks = M > 0 ? il2 + d : NULL;
   int rc = 0;
-  if (!D || !Kf || !K || !Ki || !al || !il2 || (M > 0 && !Ks)) {
-    rc = -1;
-    goto done;
-  }
   for (int p = 0; p < d; ++p) il2[p] = exp(-2.0 * theta[1 + p]);
   const double sf2 = exp(2.0 * theta[d + 1]), sn2 = exp(2.0 * theta[0]), noise = sn2 + EPS;
   /* distance stack (the KernelData pairwise per dimension), then r in order p = 1..d */
@@ -153,13 +184,6 @@ int cpufit_fit(int d, int N, int M, const double* X, const double* y, const doub
     }
   }
 done:
-  free(D);
-  free(Kf);
-  free(K);
-  free(Ki);
-  free(al);
-  free(il2);
-  free(Ks);
   return rc;
 }
 
@@ -175,25 +199,30 @@ static double now_s(void) {
  * single-fit mode).  Returns the fits completed; *seconds the elapsed wall time. */
 int cpufit_timed(int nslots, int d, int N, int M, const double* X, const double* Y, const double* T, const double* XS,
                  int threads, int blas_threads, double max_seconds, int max_fits, double* seconds) {
+  const int saved = get_threads_();
+  set_threads_(threads > 1 ? 1 : blas_threads);
   const double t0 = now_s();
   int done = 0;
-  set_threads_(threads > 1 ? 1 : blas_threads);
   double* scratch = malloc(sizeof(double) * (size_t)(threads > 0 ? threads : 1) * (3 + d + 2 * M));
 #pragma omp parallel num_threads(threads > 0 ? threads : 1)
   {
-    double* w = scratch + (size_t)omp_get_thread_num() * (3 + d + 2 * M);
-    for (;;) {
+    double* o = scratch + (size_t)omp_get_thread_num() * (3 + d + 2 * M);
+    Work w = {0, NULL};  /* this thread's workspace, allocated (and first touched) once */
+    double* ws = work_get(&w, work_need(d, N, M));
+    for (; ws;) {
       int k;
 #pragma omp atomic capture
       k = done++;
       if (k >= max_fits || now_s() - t0 > max_seconds) break;
       const int s = k % nslots;
-      cpufit_fit(d, N, M, X + (size_t)s * d * N, Y + (size_t)s * N, T + (size_t)s * (d + 2),
-                 XS ? XS + (size_t)s * d * M : NULL, w, w + 1, w + 3 + d, w + 3 + d + M);
+      fit_ws(d, N, M, X + (size_t)s * d * N, Y + (size_t)s * N, T + (size_t)s * (d + 2), XS ? XS + (size_t)s * d * M : NULL,
+             o, o + 1, o + 3 + d, o + 3 + d + M, ws);
     }
+    free(w.buf);
   }
   free(scratch);
   *seconds = now_s() - t0;
+  set_threads_(saved);
   /* every thread's last claim past the deadline or budget was not a fit */
   const int claimed = done, nthr = threads > 0 ? threads : 1;
   return claimed - nthr < 0 ? 0 : (claimed - nthr > max_fits ? max_fits : claimed - nthr);

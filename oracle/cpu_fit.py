@@ -37,6 +37,7 @@ def load():
     lib = C.CDLL(str(path))
     lib.cpufit_init.argtypes = [C.c_char_p]
     lib.cpufit_blas_threads.argtypes = [C.c_int]
+    lib.cpufit_get_blas_threads.restype = C.c_int
     dp = C.POINTER(C.c_double)
     lib.cpufit_fit.argtypes = [C.c_int, C.c_int, C.c_int, dp, dp, dp, dp, dp, dp, dp, dp]
     lib.cpufit_timed.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, dp, dp, dp, dp, C.c_int, C.c_int, C.c_double,
@@ -52,8 +53,9 @@ def _p(a):
     return a.ctypes.data_as(C.POINTER(C.c_double)) if a is not None else None
 
 
-def fit(X, y, theta, Xs=None, blas_threads: int = 1) -> dict:
-    """One fit: X (d, N), y (N,), theta (d+2,), Xs (d, M) or None -> mll, grad, mu, var."""
+def fit(X, y, theta, Xs=None, blas_threads: int | None = None) -> dict:
+    """One fit: X (d, N), y (N,), theta (d+2,), Xs (d, M) or None -> mll, grad, mu, var.
+    blas_threads: the OpenBLAS thread count for this call (restored afterwards); None keeps it."""
     lib = load()
     X = np.ascontiguousarray(X, dtype=np.float64)
     y = np.ascontiguousarray(y, dtype=np.float64)
@@ -65,8 +67,13 @@ def fit(X, y, theta, Xs=None, blas_threads: int = 1) -> dict:
     g = np.zeros(d + 2)
     mu = np.zeros(max(M, 1))
     var = np.zeros(max(M, 1))
-    lib.cpufit_blas_threads(int(blas_threads))
-    rc = lib.cpufit_fit(d, N, M, _p(X), _p(y), _p(th), _p(Xs), _p(mll), _p(g), _p(mu), _p(var))
+    saved = lib.cpufit_get_blas_threads()
+    if blas_threads is not None:
+        lib.cpufit_blas_threads(int(blas_threads))
+    try:
+        rc = lib.cpufit_fit(d, N, M, _p(X), _p(y), _p(th), _p(Xs), _p(mll), _p(g), _p(mu), _p(var))
+    finally:
+        lib.cpufit_blas_threads(saved)
     if rc != 0:
         raise RuntimeError(f"cpufit_fit: {rc}")
     out = dict(mll=float(mll[0]), grad=g)
