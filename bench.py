@@ -178,11 +178,10 @@ def cpu_baseline(X, Y, T, XT, gpu=None, max_seconds: float = 15.0, max_fits: int
         CF = None
     if impl == "c":
         if "single" in modes:
-            n, dt = CF.timed(X, Y, T, XT, threads=1, blas_threads=cores, max_seconds=max_seconds, max_fits=max_fits)
+            n, dt = CF.timed(X, Y, T, XT, threads=1, blas_threads=cores, max_seconds=max_seconds, max_fits=1 << 20)
             out["single"] = dict(value=n / dt, fits=n, seconds=round(dt, 2), blas_threads=cores)
         if "parallel" in modes:
-            n, dt = CF.timed(X, Y, T, XT, threads=cores, blas_threads=1, max_seconds=max_seconds,
-                             max_fits=max(max_fits, 16 * cores))
+            n, dt = CF.timed(X, Y, T, XT, threads=cores, blas_threads=1, max_seconds=max_seconds, max_fits=1 << 20)
             out["parallel"] = dict(value=n / dt, fits=n, seconds=round(dt, 2), threads=cores, blas_threads_each=1)
     else:
         if "single" in modes:
