@@ -120,6 +120,28 @@ def test_ragged_sizes_per_slot_inputs(gprx, ctx, N):
         check_slot(r, s, X[s], Y[s], th[s], Xs[s], ctx.dist_mode)
 
 
+@pytest.mark.parametrize("d", [1, 3, 17, 64])
+def test_input_dimension_extremes(gprx, ctx, d):
+    """d from 1 to DMAX = 64 (the Gram's 1/ell staging, the gradient epilogue's 16-dimension MFMA
+    chunks and their zero padding), ragged N, against the oracle; d = 65 is rejected."""
+    rng = np.random.default_rng(100 + d)
+    N, M, B = 130, 9, 2
+    X = rng.standard_normal((B, d, N))
+    Xs = rng.standard_normal((B, d, M))
+    Y = np.stack([np.sin(X[s].sum(axis=0)) + 0.05 * rng.standard_normal(N) for s in range(B)])
+    th = np.stack([np.concatenate([[-2.0], np.log(np.full(d, 1.5 * np.sqrt(d)) * (1 + 0.1 * rng.random(d))), [0.1]])
+                   for _ in range(B)])
+    b = gprx.GPBatch(B, d, N, M, ctx=ctx)
+    b.set_train(X, Y)
+    b.set_test(Xs)
+    r = b.run(th, grad=True, predict=True)
+    for s in range(B):
+        check_slot(r, s, X[s], Y[s], th[s], Xs[s], ctx.dist_mode)
+    b.close()
+    with pytest.raises(gprx.GPRXError):
+        gprx.GPBatch(1, 65, 64, 0, ctx=ctx)
+
+
 def test_full_size_p2_against_oracle_and_determinism(gprx, ctx):
     """BASELINE size N=2048, d=26, M=100: one slot against the oracle, and 8 slots bit-identical
     to each other and across repeated runs (size-independent properties)."""
