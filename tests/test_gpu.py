@@ -180,6 +180,32 @@ def test_not_positive_definite_status_and_pivot(gprx, ctx, golden_dir):
     check_slot(r, 1, X, Y[1], good, None, ctx.dist_mode)
 
 
+def test_overflowing_hyperparameters(gprx, ctx, golden_dir):
+    """exp overflow in the kernel parameters (Julia's exp gives Inf, as numpy's): sf2 = Inf,
+    il2 = Inf or a noise of Inf make K non-finite and the slot fails with status 1, as the oracle's
+    cholesky (dpotrf, then its finite-diagonal check); the pivot index follows LAPACK dpotf2's rule
+    (first pivot <= 0 or NaN: an Inf first pivot passes, the NaN after it fails), which for these
+    cases is the first NaN pivot, not the oracle's first non-finite diagonal.  A vanishing sf2
+    (exp(-800) = 0 + noise) stays a valid fit."""
+    z = np.load(golden_dir / "p1_n50.npz")
+    X, Y, th = z["X"], z["Y"], z["theta"]
+    b = gprx.GPBatch(1, X.shape[0], X.shape[1], 0, ctx=ctx)
+    b.set_train(X, Y[:1])
+    for i, v in [(-1, 400.0), (1, -400.0), (0, 400.0)]:
+        t = th.copy()
+        t[i] = v
+        r = b.run(t[None], grad=True)
+        with pytest.raises(O.NotPosDef):
+            O.lml(X, Y[0], t)
+        assert r["status"][0] == 1 and 1 <= r["info"][0] <= 2
+    t = th.copy()
+    t[-1] = -400.0
+    r = b.run(t[None], grad=True)
+    f = O.fit(X, Y[0], t)
+    assert r["status"][0] == 0 and abs(r["mll"][0] - f["mll"]) <= TOL_MLL * abs(f["mll"])
+    b.close()
+
+
 def test_nonfinite_theta_is_invalid_argument(gprx, ctx, golden_dir):
     z = np.load(golden_dir / "p1_n50.npz")
     b = gprx.GPBatch(2, 13, 50, 0, ctx=ctx)
