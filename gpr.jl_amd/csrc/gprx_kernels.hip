@@ -265,19 +265,23 @@ __device__ __forceinline__ void mma_64x32_s1(d4 (&acc)[WM][WN], const double* __
 // ---------------------------------------------------------------------------------------------
 // 64 x 64 wave core (k_gemm, k_lauum_grad): acc[a][b] += A(64 x K) B(64 x K)^T, same operand and
 // C maps as mma_64x32 (acc[a][b] lane l reg q = C[16a + (l&15)][16b + (l>>4) + 4q]), 16 MFMAs
-// per 8 fragment loads, two register stages in ping-pong.  ~250 VGPRs: two waves per SIMD.
-// Measured on MI355X (scratch/gemm3_bench.hip, 192 batched 1024 x 1024 panels): 70.3 TF/s at
-// K = 1024, 65.4 at K = 256, against 61.8 / 60.6 for the 64 x 32 single-stage core at 4 waves/SIMD.
+// per 8 fragment loads, two register stages of depth 8 (Q4SD = 2 MFMA sub-steps) in ping-pong,
+// ~210 VGPRs: two waves per SIMD.  Scheduling barriers pin the four phases (load stage it+1, MFMA
+// stage it, load stage it+2, MFMA stage it+1): without them the compiler sinks the prefetch next
+// to the other stage's loads and waits on vmcnt(0) before the first MFMA, serialising load and
+// compute.  Measured on MI355X (scratch/big_core_bench.hip, 192 batched 1024 x 1024 panels,
+// 2 waves/SIMD): 70.9 / 68.5 / 64.2 TF/s at K = 1024 / 512 / 256, against 64.5 / 67.4 / 63.0 for
+// depth-16 stages without the barriers (and 60.2 / 57.4 / 52.7 for depth 16 with them: 25 spills).
 // ---------------------------------------------------------------------------------------------
-constexpr int QM = 4, QN = 4;
+constexpr int QM = 4, QN = 4, Q4SD = 2;
 struct Frag4 {
-  double a[4][QM], b[4][QN];
+  double a[Q4SD][QM], b[Q4SD][QN];
 };
 // NB < QN: only the first NB 16-column blocks of B (the prediction's last, partly padded test tile)
 template <int NB = QN>
 __device__ __forceinline__ void frag4_load(Frag4& f, const double* pa, const double* pb, size_t sa, size_t sb) {
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
+  for (int s = 0; s < Q4SD; ++s) {
 #pragma unroll
     for (int a = 0; a < QM; ++a) f.a[s][a] = pa[s * sa + 16 * a];
 #pragma unroll
@@ -287,7 +291,7 @@ __device__ __forceinline__ void frag4_load(Frag4& f, const double* pa, const dou
 template <int NB = QN>
 __device__ __forceinline__ void frag4_mma(d4 (&acc)[QM][QN], const Frag4& f) {
 #pragma unroll
-  for (int s = 0; s < 4; ++s)
+  for (int s = 0; s < Q4SD; ++s)
 #pragma unroll
     for (int a = 0; a < QM; ++a)
 #pragma unroll
@@ -296,7 +300,7 @@ __device__ __forceinline__ void frag4_mma(d4 (&acc)[QM][QN], const Frag4& f) {
 template <int NB = QN>
 __device__ __forceinline__ void mma_64x64(d4 (&acc)[QM][QN], const double* __restrict__ A, size_t lda,
                                           const double* __restrict__ B, size_t ldb, int K) {
-  const int nst = __builtin_amdgcn_readfirstlane(K >> 4);  // even: K is whole 64-tiles
+  const int nst = __builtin_amdgcn_readfirstlane(K / (4 * Q4SD));  // even: K is whole 64-tiles
   if (nst <= 0) return;
   const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
   const double* pa = A + lr + (size_t)lk * lda;
@@ -305,11 +309,15 @@ __device__ __forceinline__ void mma_64x64(d4 (&acc)[QM][QN], const double* __res
   Frag4 f0, f1;
   frag4_load<NB>(f0, pa, pb, sa, sb);
   for (int it = 0; it < nst; it += 2) {
-    frag4_load<NB>(f1, pa + (size_t)(it + 1) * 4 * sa, pb + (size_t)(it + 1) * 4 * sb, sa, sb);
+    frag4_load<NB>(f1, pa + (size_t)(it + 1) * Q4SD * sa, pb + (size_t)(it + 1) * Q4SD * sb, sa, sb);
+    __builtin_amdgcn_sched_barrier(0);
     frag4_mma<NB>(acc, f0);
+    __builtin_amdgcn_sched_barrier(0);
     const int n2 = (it + 2 < nst) ? it + 2 : nst - 1;
-    frag4_load<NB>(f0, pa + (size_t)n2 * 4 * sa, pb + (size_t)n2 * 4 * sb, sa, sb);
+    frag4_load<NB>(f0, pa + (size_t)n2 * Q4SD * sa, pb + (size_t)n2 * Q4SD * sb, sa, sb);
+    __builtin_amdgcn_sched_barrier(0);
     frag4_mma<NB>(acc, f1);
+    __builtin_amdgcn_sched_barrier(0);
   }
 }
 __device__ __forceinline__ void acc4_zero(d4 (&acc)[QM][QN]) {

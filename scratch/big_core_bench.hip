@@ -48,8 +48,32 @@ __device__ __forceinline__ void core(d4 (&acc)[WM][WN], const double* A, size_t 
   }
 }
 
-// WG = 4 waves (2 x 2), wave tile (16 WM) x (16 WN); WG tile (32 WM) x (32 WN).
+// the same core with scheduling barriers between the four phases: the prefetch of stage it+1 stays
+// in flight across the MFMAs of stage it (the compiler otherwise sinks the loads and waits on all)
 template <int WM, int WN, int SD>
+__device__ __forceinline__ void core_sb(d4 (&acc)[WM][WN], const double* A, size_t lda, const double* B, size_t ldb, int K) {
+  const int nst = __builtin_amdgcn_readfirstlane(K / (4 * SD));
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  const double* pa = A + lr + (size_t)lk * lda;
+  const double* pb = B + lr + (size_t)lk * ldb;
+  const size_t sa = 4 * lda, sb = 4 * ldb;
+  Frag<WM, WN, SD> f0, f1;
+  fload(f0, pa, pb, sa, sb);
+  for (int it = 0; it < nst; it += 2) {
+    fload(f1, pa + (size_t)(it + 1) * SD * sa, pb + (size_t)(it + 1) * SD * sb, sa, sb);
+    __builtin_amdgcn_sched_barrier(0);
+    fmma(acc, f0);
+    __builtin_amdgcn_sched_barrier(0);
+    const int n2 = (it + 2 < nst) ? it + 2 : nst - 1;
+    fload(f0, pa + (size_t)n2 * SD * sa, pb + (size_t)n2 * SD * sb, sa, sb);
+    __builtin_amdgcn_sched_barrier(0);
+    fmma(acc, f1);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// WG = 4 waves (2 x 2), wave tile (16 WM) x (16 WN); WG tile (32 WM) x (32 WN).
+template <int WM, int WN, int SD, bool SB = false>
 __device__ __forceinline__ void body(const double* P, double* C, int T, int nbr, int K, int S) {
   const int x = blockIdx.x & 7, q = blockIdx.x >> 3;
   const int slot = (q / T) * 8 + x, u = q % T;
@@ -63,7 +87,8 @@ __device__ __forceinline__ void body(const double* P, double* C, int T, int nbr,
 #pragma unroll
     for (int b = 0; b < WN; ++b) acc[a][b] = (d4){0, 0, 0, 0};
   const int r0 = 1024 + bi * 32 * WM + 16 * WM * wr, c0 = bj * 32 * WN + 16 * WN * wc;
-  core<WM, WN, SD>(acc, M + r0, 2048, M + c0, 2048, K);
+  if constexpr (SB) core_sb<WM, WN, SD>(acc, M + r0, 2048, M + c0, 2048, K);
+  else core<WM, WN, SD>(acc, M + r0, 2048, M + c0, 2048, K);
   double* Cs = C + (size_t)slot * 1024 * 1024;
   const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
 #pragma unroll
@@ -80,6 +105,14 @@ __device__ __forceinline__ void body(const double* P, double* C, int T, int nbr,
     body<WM, WN, SD>(P, C, T, nbr, K, S);                                                             \
   }
 KERN(k_64x64_sd4_o2, 4, 4, 4, 2)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_64x64_sb_o2(
+    const double* P, double* C, int T, int nbr, int K, int S) {
+  body<4, 4, 4, true>(P, C, T, nbr, K, S);
+}
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_64x64_sb2_o2(
+    const double* P, double* C, int T, int nbr, int K, int S) {
+  body<4, 4, 2, true>(P, C, T, nbr, K, S);
+}
 KERN(k_128x64_sd2_o2, 8, 4, 2, 2)
 KERN(k_128x64_sd4_o1, 8, 4, 4, 1)
 KERN(k_128x128_sd2_o1, 8, 8, 2, 1)
@@ -101,10 +134,9 @@ int main() {
   (void)hipEventCreate(&e1);
   struct V { const char* name; const void* f; int WM, WN; };
   V vs[] = {{"64x64 sd4 o2 (library)", (const void*)k_64x64_sd4_o2, 4, 4},
-            {"128x64 sd2 o2", (const void*)k_128x64_sd2_o2, 8, 4},
-            {"128x64 sd4 o1", (const void*)k_128x64_sd4_o1, 8, 4},
-            {"128x128 sd2 o1", (const void*)k_128x128_sd2_o1, 8, 8},
-            {"128x128 sd1 o1", (const void*)k_128x128_sd1_o1, 8, 8}};
+            {"64x64 sd4 o2 sched-barrier", (const void*)k_64x64_sb_o2, 4, 4},
+            {"64x64 sd2 o2 sched-barrier", (const void*)k_64x64_sb2_o2, 4, 4},
+            {"128x64 sd4 o1", (const void*)k_128x64_sd4_o1, 8, 4}};
   for (int K : {1024, 512, 256}) {
     bool first = true;
     for (auto& v : vs) {
