@@ -458,8 +458,7 @@ int gprx_batch_create(gprx_ctx* c, int B, int d, int N, int M_max, gprx_batch** 
   db.mat = (size_t)db.Npad * db.Npad;
   db.pst = d + 4;
   db.gps = d + 2;
-  db.ngu = gprx::lauum_units(db.nt);
-  db.nlj = gprx::lauum_jobs(db.nt);
+  db.nlj = gprx::lauum_plan(db.nt, d, &db.ngu, &db.nimg, nullptr);
   const size_t Bs = B;
   int rc = GPRX_OK;
   auto fail = [&](int r) {  // under c->mu: unlink here, free without re-locking
@@ -467,8 +466,9 @@ int gprx_batch_create(gprx_ctx* c, int B, int d, int N, int M_max, gprx_batch** 
     batch_free(b);
     return r;
   };
+  if (db.nlj < 1) return fail(set_err(c, GPRX_INVALID_ARGUMENT, "gprx_batch_create: lauum plan failed"));
   if ((rc = dalloc(b, &db.X, Bs * db.Npad * d))) return fail(rc);
-  db.xs = 16 * ((d + 15) / 16) + 1;
+  db.xs = d | 1;
   if ((rc = dalloc(b, &db.Xc, Bs * db.Npad * db.xs))) return fail(rc);
   if ((rc = dalloc(b, &db.Y, Bs * db.Npad))) return fail(rc);
   if ((rc = dalloc(b, &db.K, Bs * db.mat))) return fail(rc);
@@ -485,11 +485,12 @@ int gprx_batch_create(gprx_ctx* c, int B, int d, int N, int M_max, gprx_batch** 
   if ((rc = dalloc(b, &db.out, Bs * (d + 3)))) return fail(rc);
   if ((rc = dalloc(b, &db.status, 2 * Bs))) return fail(rc);
   db.info = db.status + Bs;
-  if ((rc = dalloc(b, &db.lauum_order, 6 * (size_t)db.nlj))) return fail(rc);
+  if ((rc = dalloc(b, &db.lauum_order, 2 * gprx::LU * (size_t)db.nlj))) return fail(rc);
   if ((rc = dalloc(b, &b->opt_active, Bs))) return fail(rc);
   {
-    std::vector<int> ord(6 * (size_t)db.nlj);
-    gprx::lauum_order_host(db.nt, ord.data());
+    std::vector<int> ord(2 * gprx::LU * (size_t)db.nlj);
+    int nu, ni;
+    gprx::lauum_plan(db.nt, d, &nu, &ni, ord.data());
     if (hipMemcpy(db.lauum_order, ord.data(), ord.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess)
       return fail(GPRX_DEVICE_ERROR);
   }

@@ -28,11 +28,12 @@ struct DevBatch {
   int small_n;                 // recursion nodes of <= small_n tiles use the 64 x 32 pair-unit GEMM
                                // (default 8 for B >= 32, all nodes below that, where the 64 x 64
                                // units leave most of the chip idle); larger: 64 x 64 core
-  int xs;                      // row stride of Xc: 16 ceil(d/16) + 1 (odd: spreads LDS banks)
+  int xs;                      // row stride of Xc: d | 1 (odd: spreads LDS banks)
   int pst;                     // stride of params per slot
   int gps;                     // stride of per-unit gradient partials (d + 2)
-  int ngu;                     // gradient partial units per slot (lauum 2 x 2-tile units)
+  int ngu;                     // gradient partial units per slot (lauum 4-tile units)
   int nlj;                     // lauum jobs per slot (units folded in pairs)
+  int nimg;                    // largest number of point-tile images of a lauum unit (LDS size)
   size_t ld, mat;              // ld = Npad, mat = Npad*Npad
   double* X;                   // B x [Npad][d]   (column t = one CState, contiguous d values)
   double* Xc;                  // B x [Npad][xs]  X minus its per-dimension mean over the N points,
@@ -61,7 +62,7 @@ struct DevBatch {
   double* out_var;             // B x Mpad
   int* status;                 // B
   int* info;                   // B
-  int* lauum_order;            // nlj x 6: two (first row, first column, unit id) per job, long + short
+  int* lauum_order;            // nlj x 2 x LU: two units per job, long + short (lauum_plan)
   const int* active;           // B or null: evaluate only the slots with active[s] != 0 (the device
                                //   optimiser's rounds; null = every slot)
 };
@@ -211,9 +212,11 @@ void launch_leaf(const DevBatch& b, int o, int n, hipStream_t s);
 void launch_gemm(const DevBatch& b, const GemmGeom& g, hipStream_t s, const GemmGeom& g2 = GemmGeom{OP_NONE, 0, 0, 0});
 void launch_alpha(const DevBatch& b, hipStream_t s, int phase);
 void launch_lauum_grad(const DevBatch& b, hipStream_t s);
-int lauum_units(int nt);
-int lauum_jobs(int nt);
-void lauum_order_host(int nt, int* out);
+// k_lauum_grad's job table: units of 4 output tiles, folded in pairs; LU ints per unit (see
+// lauum_plan in gprx_kernels.hip).  Returns the jobs per slot; *nunits the units, *nimg the
+// largest image count; out (nullable) receives jobs x 2 x LU ints.
+constexpr int LU = 24;
+int lauum_plan(int nt, int d, int* nunits, int* nimg, int* out);
 void launch_finalize(const DevBatch& b, int want_grad, hipStream_t s);
 void launch_pred_cross(const DevBatch& b, hipStream_t s);
 void launch_pred_mu(const DevBatch& b, hipStream_t s);

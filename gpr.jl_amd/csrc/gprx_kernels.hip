@@ -21,6 +21,8 @@
 // Workgroup -> (slot, unit) mapping keeps every slot's units on one XCD (blocks b, b+8, ... share
 // an XCD), so the panels of a slot stay in that XCD's L2.
 #include "gprx_internal.h"
+#include <algorithm>
+#include <array>
 #include <cstdlib>
 #include <vector>
 
@@ -1239,7 +1241,7 @@ __global__ __launch_bounds__(NTHR) void k_alpha(DevBatch db, int phase) {
 //   G_rc = wt_rc * (alpha_r alpha_c - Kinv_rc) * Kf_rc    (wt = 1/2 on the diagonal, as
 //                                                        dmll_kern! weights ααinvcKI[j,j]/2)
 //   S_p = sum G_rc (x_pr - x_pc)^2,  S_f = sum G_rc,  T = sum_diag W_rr
-// Unit = tile pair (ti, ti+1) x tj of the lower triangle; one gradient partial row per unit.
+// One gradient partial row per unit of 4 tiles.
 //
 // The distance sums are expanded per wave tile (rows r, columns c):
 //   S_p = sum_r x_pr^2 R_r + sum_c x_pc^2 C_c - 2 sum_r x_pr Q_rp,   Q = G Xc  (64 x d)
@@ -1249,8 +1251,8 @@ __global__ __launch_bounds__(NTHR) void k_alpha(DevBatch db, int phase) {
 // 32 d distance evaluations and d wave reductions.  x is the centred copy Xc (per-dimension mean
 // removed; S_p is translation invariant), which keeps the expansion's cancellation at the
 // rounding level of the points' spread, as for the reference's own a^2 + b^2 - 2ab distances.
-// LDS: the unit's three point tiles as raw [point][d] images (LDS-DMA, issued before the MFMA
-// loop), then 4 x 64 per-wave partials.
+// LDS: the unit's point tiles as raw [point][xs] images (LDS-DMA, issued before the MFMA loop),
+// per-wave partials, norms and alpha of the image points.
 // ============================================================================================
 __device__ __forceinline__ void dma_tile(double* lds, const double* src, int ndbl) {
   // ndbl doubles (even) from src to lds, 16 B per lane, one wave-instruction per KiB;
@@ -1263,40 +1265,50 @@ __device__ __forceinline__ void dma_tile(double* lds, const double* src, int ndb
   }
 }
 constexpr int SPW = DMAX + 2;  // per-wave partial row: S_p (d), S_f, T
-// Unit = 2 x 2 tiles (pr, pr+1) x (pc, pc+1) of the lower triangle; wave (wr, wc) = tile
-// (pr + wr, pc + wc) if on or below the diagonal.  LDS: the unit's four point tiles (raw [64][xs]
-// images, LDS-DMA before the MFMA loop), per-wave partials, the points' weighted norms, alpha and
-// il2.
-__device__ __forceinline__ void lauum_unit(const DevBatch& db, int slot, int pr, int pc, int u);
+// LDS of a lauum workgroup: per-wave partials, the images' weighted squared norms and alpha, il2,
+// then nimg point-tile images [64][xs] (16-B aligned: the small arrays hold an even count)
+static_assert((4 * SPW + 2 * 5 * TS + DMAX) % 2 == 0, "lauum LDS image base alignment");
+__host__ __device__ inline size_t lauum_lds_dbl(int xs, int nimg) {
+  return (size_t)4 * SPW + 2 * 5 * TS + DMAX + (size_t)nimg * TS * xs;
+}
+// Unit = 4 output tiles of the lower triangle, one per wave, each with its own K range [ti, nt)
+// (register-direct operands: the waves share no panel, only the unit's point-tile images for the
+// epilogue).  Job table entry per unit (LU ints):
+//   [0] unit id (-1: none)  [1] nimg  [2..6] image tiles  [7..10] ti per wave (-1: idle)
+//   [11..14] tj  [15..18] image of ti  [19..22] image of tj
+// The plan (lauum_plan) takes the lower tiles in row order, four consecutive tiles per unit: the
+// waves' K ranges differ by at most one tile (99% of the wave time is MFMA work at nt = 32,
+// against 92% for 2 x 2 units, whose diagonal units leave a wave idle and whose second tile row
+// has 64 less K).  Such a unit needs up to 5 images (row tiles and column tiles); where 5 images
+// would cost a workgroup per CU against 4 (d > 26 at two per CU, d > 63 at one), the plan falls
+// back to 2 x 2 units.
+__device__ __forceinline__ void lauum_unit(const DevBatch& db, int slot, const int* ju);
 __device__ __forceinline__ void lauum_body(const DevBatch& db) {
   int slot, job;
   if (!map_slot(db, db.nlj, slot, job)) return;
-  const int* jb = db.lauum_order + 6 * job;
-  lauum_unit(db, slot, jb[0], jb[1], jb[2]);
-  if (jb[3] >= 0) {  // block-uniform: the folded short unit
+  const int* jb = db.lauum_order + (size_t)job * 2 * LU;
+  lauum_unit(db, slot, jb);
+  if (jb[LU] >= 0) {  // block-uniform: the folded short unit
     __syncthreads();  // the first unit's LDS images and partials are consumed
-    lauum_unit(db, slot, jb[3], jb[4], jb[5]);
+    lauum_unit(db, slot, jb + LU);
   }
 }
-__device__ __forceinline__ void lauum_unit(const DevBatch& db, int slot, int pr, int pc, int u) {
+__device__ __forceinline__ void lauum_unit(const DevBatch& db, int slot, const int* ju) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  const int d = db.d, tid = threadIdx.x, w = tid >> 6, wr = w >> 1, wc = w & 1;
-  const int xs = db.xs, xt = TS * xs;  // point-tile image: [64][xs], dims >= d zero
-  double* xr_s = sm;                    // [2][64][xs] rows of tiles pr, pr+1
-  double* xc_s = sm + 2 * xt;           // [2][64][xs] rows of tiles pc, pc+1
-  double* sp = sm + 4 * xt;             // [4][SPW]
-  double* nrm = sp + 4 * SPW;           // [4][64] weighted squared norms (tiles pr, pr+1, pc, pc+1)
-  double* als = nrm + 4 * TS;           // [4][64] alpha of the same points
-  double* wl = als + 4 * TS;            // [DMAX] il2
+  const int d = db.d, tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int xs = db.xs, xt = TS * xs;  // point-tile image: [64][xs]
+  const int nimg = ju[1];
+  double* sp = sm;                      // [4][SPW]
+  double* nrm = sp + 4 * SPW;           // [nimg][64] weighted squared norms of the image points
+  double* als = nrm + 5 * TS;           // [nimg][64] alpha of the same points
+  double* wl = als + 5 * TS;            // [DMAX] il2
+  double* img = wl + DMAX;              // [nimg][64][xs]
   const int nt = db.nt;
   const double* X = db.Xc + (size_t)slot * db.Npad * xs;
   const double* al = db.alpha + (size_t)slot * db.Npad;
-  dma_tile(xr_s, X + (size_t)pr * xt, xt);
-  if (pr + 1 < nt) dma_tile(xr_s + xt, X + (size_t)(pr + 1) * xt, xt);
-  dma_tile(xc_s, X + (size_t)pc * xt, xt);
-  if (pc + 1 < nt) dma_tile(xc_s + xt, X + (size_t)(pc + 1) * xt, xt);
-  const int ti = pr + wr, tj = pc + wc;
-  const bool active = ti < nt && tj <= ti;
+  for (int i = 0; i < nimg; ++i) dma_tile(img + i * xt, X + (size_t)ju[2 + i] * xt, xt);
+  const int ti = ju[7 + w], tj = ju[11 + w];
+  const bool active = ti >= 0;
   const int l = tid & 63, lr = l & 15, lk = l >> 4;
   d4 acc[QM][QN];
   acc4_zero(acc);
@@ -1311,25 +1323,23 @@ __device__ __forceinline__ void lauum_unit(const DevBatch& db, int slot, int pr,
   for (int e = l; e < SPW; e += 64) spw[e] = 0.0;
   const double* P = db.params + (size_t)slot * db.pst;
   if (tid < d) wl[tid] = P[tid];
-  {  // one point per thread: weighted squared norm and alpha (points of missing tiles: 0)
-    const int t4 = tid >> 6, pt = tid & 63;
-    const int tile = (t4 < 2 ? pr : pc) + (t4 & 1);
-    const double* xp = sm + (size_t)tid * xs;
+  for (int e = tid; e < nimg * TS; e += NTHR) {  // one image point per thread
+    const double* xp = img + (size_t)e * xs;
     double nn = 0.0;
-    if (tile < nt)
-      for (int p = 0; p < d; ++p) nn = fma(P[p] * xp[p], xp[p], nn);
-    nrm[tid] = nn;
-    als[tid] = tile < nt ? al[tile * TS + pt] : 0.0;
+    for (int p = 0; p < d; ++p) nn = fma(P[p] * xp[p], xp[p], nn);
+    nrm[e] = nn;
+    als[e] = al[ju[2 + (e >> 6)] * TS + (e & 63)];
   }
   __syncthreads();
   if (active) {
     const double sf2 = P[d];
-    const double* xr = xr_s + wr * xt;  // [r][xs]
-    const double* xc = xc_s + wc * xt;  // [c][xs]
-    const double* nr = nrm + wr * TS;
-    const double* nc = nrm + (2 + wc) * TS;
-    const double* ar = als + wr * TS;
-    const double* ac = als + (2 + wc) * TS;
+    const int ir = ju[15 + w], ic = ju[19 + w];
+    const double* xr = img + ir * xt;  // [r][xs]
+    const double* xc = img + ic * xt;  // [c][xs]
+    const double* nr = nrm + ir * TS;
+    const double* nc = nrm + ic * TS;
+    const double* ar = als + ir * TS;
+    const double* ac = als + ic * TS;
     const int KS = (d + 3) >> 2;
     // G in place of acc:  Kf recomputed from r = n_r + n_c - 2 sum_p il2_p xc_pr xc_pc (MFMA, one
     // 16 x 16 block at a time; the same centred points as the distance sums below)
@@ -1344,10 +1354,13 @@ __device__ __forceinline__ void lauum_unit(const DevBatch& db, int slot, int pr,
 #pragma unroll
       for (int s2 = 0; s2 < (DMAX + 3) / 4; ++s2) {
         if (s2 < KS) {
-          const int k = 4 * s2 + lk;
-          const double xa = wl[k < d ? k : 0] * xr[(16 * a + lr) * xs + k];  // xr = 0 for k >= d
+          // dimensions k >= d (the last step's padding): the A operand is zero, the B operand a
+          // finite image value (clamped index)
+          const int k = 4 * s2 + lk, kc = k < d ? k : d - 1;
+          const double xv = wl[kc] * xr[(16 * a + lr) * xs + kc];
+          const double xa = k < d ? xv : 0.0;
 #pragma unroll
-          for (int b = 0; b < QN; ++b) cr4[b] = mfma(xc[(16 * b + lr) * xs + k], xa, cr4[b]);
+          for (int b = 0; b < QN; ++b) cr4[b] = mfma(xc[(16 * b + lr) * xs + kc], xa, cr4[b]);
         }
       }
 #pragma unroll
@@ -1402,15 +1415,16 @@ __device__ __forceinline__ void lauum_unit(const DevBatch& db, int slot, int pr,
     const int H = (d + 15) >> 4;
 #pragma unroll 1
     for (int h = 0; h < H; ++h) {
-      // A operand: x of column point c = 16b + 4q + lk, dimension pA = 16h + lr
-      const int pA = 16 * h + lr;
+      // A operand: x of column point c = 16b + 4q + lk, dimension pA = 16h + lr (clamped to a
+      // finite image value for pA >= d: those Q columns and t2 lanes are never stored)
+      const int pA = 16 * h + lr, pAc = pA < d ? pA : d - 1;
       double xa[QN][4];
       double t2 = 0.0;  // sum_c x_{pA,c}^2 C_c over this lane's 16 columns
 #pragma unroll
       for (int b = 0; b < QN; ++b)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          xa[b][q] = xc[(16 * b + 4 * q + lk) * xs + pA];
+          xa[b][q] = xc[(16 * b + 4 * q + lk) * xs + pAc];
           t2 = fma(xa[b][q] * xa[b][q], Cs[b][q], t2);
         }
       double t13[4] = {0.0, 0.0, 0.0, 0.0};  // dims p = 16h + lk + 4q'
@@ -1424,7 +1438,8 @@ __device__ __forceinline__ void lauum_unit(const DevBatch& db, int slot, int pr,
         // lane: row r = 16a + lr; Q[q'] = Q[r][16h + lk + 4q']
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq) {
-          const double x = xr[(16 * a + lr) * xs + 16 * h + lk + 4 * qq];
+          const int p = 16 * h + lk + 4 * qq;
+          const double x = xr[(16 * a + lr) * xs + (p < d ? p : d - 1)];
           t13[qq] = fma(x, fma(x, R[a], -2.0 * Q[qq]), t13[qq]);
         }
       }
@@ -1458,32 +1473,87 @@ __device__ __forceinline__ void lauum_unit(const DevBatch& db, int slot, int pr,
     spw[d + 1] = tr;
   }
   __syncthreads();
-  double* out = db.grad_part + ((size_t)slot * db.ngu + u) * db.gps;
+  double* out = db.grad_part + ((size_t)slot * db.ngu + ju[0]) * db.gps;
   for (int e = tid; e < d + 2; e += NTHR)
     out[e] = ((sp[e] + sp[SPW + e]) + sp[2 * SPW + e]) + sp[3 * SPW + e];
 }
 __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_lauum_grad(DevBatch db) {
   lauum_body(db);
 }
-int lauum_units(int nt) { return quad_units(nt, nt, true); }
-int lauum_jobs(int nt) { return (lauum_units(nt) + 1) / 2; }
-void lauum_order_host(int nt, int* out) {
-  // 2 x 2-tile units of the lower triangle (first row, first column, unit id), K range [row, nt);
-  // folded into jobs of two: the i-th longest with the i-th shortest (then the middle one alone),
-  // jobs in decreasing order of their long unit.  6 ints per job; pr = -1 marks no second unit.
-  std::vector<int> us;
-  for (int rp = 0; 2 * rp < nt; ++rp)
-    for (int cp = 0; cp <= rp; ++cp) us.push_back(2 * rp), us.push_back(2 * cp);
-  const int n = (int)us.size() / 2, nj = lauum_jobs(nt);
-  for (int j = 0; j < nj; ++j) {
-    const int a = j, b = nj == n ? j : n - 1 - j;  // units are already in decreasing K order
-    out[6 * j + 0] = us[2 * a];
-    out[6 * j + 1] = us[2 * a + 1];
-    out[6 * j + 2] = a;
-    out[6 * j + 3] = (b != a) ? us[2 * b] : -1;
-    out[6 * j + 4] = (b != a) ? us[2 * b + 1] : -1;
-    out[6 * j + 5] = (b != a) ? b : -1;
+// workgroups per CU that an LDS size allows (2 at most: the kernel's VGPRs)
+static int lauum_wgs(size_t bytes) {
+  const size_t cu = 160 * 1024;
+  return bytes > cu ? 0 : (int)std::min<size_t>(2, cu / bytes);
+}
+int lauum_plan(int nt, int d, int* nunits, int* nimg, int* out) {
+  const int xs = d | 1;
+  const size_t b4 = lauum_lds_dbl(xs, 4) * sizeof(double), b5 = lauum_lds_dbl(xs, 5) * sizeof(double);
+  const bool rows = lauum_wgs(b5) >= lauum_wgs(b4) && lauum_wgs(b5) > 0;
+  // units in decreasing K order (K = nt - first row), each as its 4 (ti, tj) (ti = -1: idle wave)
+  std::vector<std::array<int, 8>> us;
+  if (rows) {
+    std::vector<std::pair<int, int>> t;
+    for (int i = 0; i < nt; ++i)
+      for (int j = 0; j <= i; ++j) t.push_back({i, j});
+    for (size_t k = 0; k < t.size(); k += 4) {
+      std::array<int, 8> u;
+      for (int w = 0; w < 4; ++w) {
+        const bool in = k + w < t.size();
+        u[w] = in ? t[k + w].first : -1;
+        u[4 + w] = in ? t[k + w].second : -1;
+      }
+      us.push_back(u);
+    }
+  } else {
+    for (int pr = 0; pr < nt; pr += 2)
+      for (int pc = 0; pc <= pr; pc += 2) {
+        std::array<int, 8> u;
+        for (int w = 0; w < 4; ++w) {
+          const int i = pr + (w >> 1), j = pc + (w & 1);
+          const bool in = i < nt && j <= i;
+          u[w] = in ? i : -1;
+          u[4 + w] = in ? j : -1;
+        }
+        us.push_back(u);
+      }
   }
+  const int n = (int)us.size(), nj = (n + 1) / 2;
+  *nunits = n;
+  *nimg = 0;
+  auto fill = [&](int* e, int id) {  // one LU-int entry of unit id (-1: none)
+    for (int k = 0; k < LU; ++k) e[k] = -1;
+    if (id < 0) return;
+    const std::array<int, 8>& u = us[id];
+    int img[8], ni = 0;
+    auto slot_of = [&](int tile) {
+      for (int k = 0; k < ni; ++k)
+        if (img[k] == tile) return k;
+      img[ni] = tile;
+      return ni++;
+    };
+    e[0] = id;
+    for (int w = 0; w < 4; ++w) {
+      e[7 + w] = u[w];
+      e[11 + w] = u[4 + w];
+      if (u[w] >= 0) {
+        e[15 + w] = slot_of(u[w]);
+        e[19 + w] = slot_of(u[4 + w]);
+      }
+    }
+    e[1] = ni;  // <= 5: at most 2 row tiles (2 x 2: 2 rows, 2 columns) and 4 column tiles
+    for (int k = 0; k < ni && k < 5; ++k) e[2 + k] = img[k];
+    if (ni > 5) e[1] = -1;  // not reached; lauum_plan returns -1
+    *nimg = std::max(*nimg, ni);
+  };
+  std::vector<int> tmp(2 * LU);
+  for (int j = 0; j < nj; ++j) {
+    const int a = j, b = (n - 1 - j != j) ? n - 1 - j : -1;  // the j-th longest + the j-th shortest
+    int* e = out ? out + (size_t)j * 2 * LU : tmp.data();
+    fill(e, a);
+    fill(e + LU, b);
+    if (e[1] < 0 || (b >= 0 && e[LU + 1] < 0)) return -1;
+  }
+  return nj;
 }
 
 // ============================================================================================
@@ -1761,9 +1831,7 @@ __global__ __launch_bounds__(NT) void k_rollout(RolloutArgs a) {
 // launchers
 // ---------------------------------------------------------------------------------------------
 static size_t gram_lds(int d) { return (size_t)(2 * d * TS + 2 * DMAX + 4) * sizeof(double); }
-static size_t lauum_lds(int d) {
-  return (size_t)(4 * (16 * ((d + 15) / 16) + 1) * TS + 4 * SPW + 8 * TS + DMAX) * sizeof(double);
-}
+static size_t lauum_lds(const DevBatch& b) { return lauum_lds_dbl(b.xs, b.nimg) * sizeof(double); }
 static size_t cross_lds(int d) { return (size_t)(2 * d * TS + 2 * DMAX + 4) * sizeof(double); }
 
 static void set_lds_limits() {
@@ -1772,7 +1840,7 @@ static void set_lds_limits() {
   done = true;
   for (const void* f : {(const void*)k_gram<0>, (const void*)k_gram<1>})
     (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)gram_lds(DMAX));
-  (void)hipFuncSetAttribute((const void*)k_lauum_grad, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lauum_lds(DMAX));
+  (void)hipFuncSetAttribute((const void*)k_lauum_grad, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   for (const void* f : {(const void*)k_pred_cross<0>, (const void*)k_pred_cross<1>})
     (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)cross_lds(DMAX));
 }
@@ -1812,7 +1880,7 @@ void launch_alpha(const DevBatch& b, hipStream_t s, int phase) {
 }
 void launch_lauum_grad(const DevBatch& b, hipStream_t s) {
   set_lds_limits();
-  hipLaunchKernelGGL(k_lauum_grad, dim3(grid_blocks(b.B, b.nlj)), dim3(NTHR), lauum_lds(b.d), s, b);
+  hipLaunchKernelGGL(k_lauum_grad, dim3(grid_blocks(b.B, b.nlj)), dim3(NTHR), lauum_lds(b), s, b);
 }
 void launch_finalize(const DevBatch& b, int want_grad, hipStream_t s) {
   hipLaunchKernelGGL(k_finalize, dim3(b.B), dim3(NTHR), 0, s, b, want_grad);
