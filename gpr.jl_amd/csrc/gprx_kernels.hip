@@ -368,13 +368,10 @@ __host__ __device__ inline void unit_shape(int op, int& UR, int& UC) {
   UR = op == OP_TRSM ? 4 : ((op == OP_TT || op == OP_LINV21) ? 1 : 2);
   UC = 4 / UR;
 }
-// rect R x C: ceil(R/UR) x ceil(C/UC) units; lower triangle of R x R (tri, 2 x 2 only): row pair
-// RP holds column pairs 0..RP.
+// rect R x C: ceil(R/UR) x ceil(C/UC) units; lower triangle of R x R (tri: SYRK, fixed K): four
+// consecutive tiles of the row-major lower triangle per unit (no idle wave on the diagonal)
 __host__ __device__ inline int quad_units(int R, int C, bool tri, int UR = 2, int UC = 2) {
-  if (tri) {
-    const int RP = (R + 1) / 2;
-    return RP * (RP + 1) / 2;
-  }
+  if (tri) return (R * (R + 1) / 2 + 3) / 4;
   return ((R + UR - 1) / UR) * ((C + UC - 1) / UC);
 }
 // Triangular-K ops are folded: a workgroup computes the unit with the longest K range and then
@@ -718,9 +715,9 @@ __device__ __forceinline__ void diag_tile_fast(const DevBatch& db, int slot, int
 
 
 // ============================================================================================
-// Generic batched tile GEMM of the recursion (see GemmOp).  Unit = 2 x 2 output tiles; wave
-// (wr, wc) computes tile (pr + wr, pc + wc), 64 x 64, with its own K range (triangular operands
-// are skipped at tile granularity).  Waves of tiles outside the rectangle / above the diagonal
+// Generic batched tile GEMM of the recursion (see GemmOp).  Unit = 4 output tiles (unit_shape;
+// a triangular SYRK: 4 consecutive lower tiles); each wave computes one 64 x 64 tile with its own
+// K range (triangular operands are skipped at tile granularity).  Waves of tiles outside the rectangle / above the diagonal
 // return at once (no workgroup barrier in this kernel).
 // ============================================================================================
 // One 64 x 64 output tile (ti, tj) of a GemmOp on one wave.
@@ -840,10 +837,14 @@ __device__ __forceinline__ void gemm_body(const DevBatch& db, const GemmGeom& g1
   int UR, UC;
   unit_shape(op, UR, UC);
   int np = 1, pr2 = 0, pc2 = 0;  // second (folded) unit
-  if (tri) {
-    quad_tri(u, pr, pc);
-    pr *= 2;
-    pc *= 2;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (tri) {  // lower-triangle tile 4u + w in row-major order
+    const int t = 4 * u + w;
+    if (t >= R * (R + 1) / 2) return;  // wave-uniform: the last unit's missing tiles
+    int i, j;
+    quad_tri(t, i, j);
+    gemm_tile<PV>(db, g, slot, __builtin_amdgcn_readfirstlane(r0 + i), __builtin_amdgcn_readfirstlane(c0 + j));
+    return;
   } else {
     const int RU = (R + UR - 1) / UR, CU = (C + UC - 1) / UC;
     if (op == OP_SYRK) {
@@ -864,12 +865,11 @@ __device__ __forceinline__ void gemm_body(const DevBatch& db, const GemmGeom& g1
       np = (lo != hi) ? 2 : 1;
     }
   }
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), wr = w / UC, wc = w - wr * UC;
+  const int wr = w / UC, wc = w - wr * UC;
 #pragma unroll 1
   for (int pass = 0; pass < np; ++pass) {
     const int ur = pass ? pr2 : pr, uc = pass ? pc2 : pc;
     if (ur + wr >= R || uc + wc >= C) continue;  // wave-uniform: partial unit
-    if (tri && uc + wc > ur + wr) continue;      // above the diagonal
     // wave-uniform tile indices in SGPRs (the 64 x 64 core needs every VGPR)
     gemm_tile<PV>(db, g, slot, __builtin_amdgcn_readfirstlane(r0 + ur + wr), __builtin_amdgcn_readfirstlane(c0 + uc + wc));
   }
