@@ -322,6 +322,48 @@ __device__ __forceinline__ void mma_64x64(d4 (&acc)[QM][QN], const double* __res
     __builtin_amdgcn_sched_barrier(0);
   }
 }
+// 64 x 16 wave core (the fused leaf's column-quarter tasks): acc[a] += A(64 x K) B(16 x K)^T,
+// lane l reg q = C[16a + (l&15)][(l>>4) + 4q]; 4 MFMAs per 5 fragment loads, stages of depth 16
+// in ping-pong (the same phase barriers as mma_64x64).  K: whole 64-tiles.
+struct Frag16 {
+  double a[4][QM], b[4];
+};
+__device__ __forceinline__ void frag16_load(Frag16& f, const double* pa, const double* pb, size_t sa, size_t sb) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+#pragma unroll
+    for (int a = 0; a < QM; ++a) f.a[s][a] = pa[s * sa + 16 * a];
+    f.b[s] = pb[s * sb];
+  }
+}
+__device__ __forceinline__ void frag16_mma(d4 (&acc)[QM], const Frag16& f) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int a = 0; a < QM; ++a) acc[a] = mfma(f.b[s], f.a[s][a], acc[a]);
+}
+__device__ __forceinline__ void mma_64x16(d4 (&acc)[QM], const double* __restrict__ A, size_t lda,
+                                          const double* __restrict__ B, size_t ldb, int K) {
+  const int nst = __builtin_amdgcn_readfirstlane(K >> 4);  // even: K is whole 64-tiles
+  if (nst <= 0) return;
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  const double* pa = A + lr + (size_t)lk * lda;
+  const double* pb = B + lr + (size_t)lk * ldb;
+  const size_t sa = 4 * lda, sb = 4 * ldb;
+  Frag16 f0, f1;
+  frag16_load(f0, pa, pb, sa, sb);
+  for (int it = 0; it < nst; it += 2) {
+    frag16_load(f1, pa + (size_t)(it + 1) * 4 * sa, pb + (size_t)(it + 1) * 4 * sb, sa, sb);
+    __builtin_amdgcn_sched_barrier(0);
+    frag16_mma(acc, f0);
+    __builtin_amdgcn_sched_barrier(0);
+    const int n2 = (it + 2 < nst) ? it + 2 : nst - 1;
+    frag16_load(f0, pa + (size_t)n2 * 4 * sa, pb + (size_t)n2 * 4 * sb, sa, sb);
+    __builtin_amdgcn_sched_barrier(0);
+    frag16_mma(acc, f1);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
 __device__ __forceinline__ void acc4_zero(d4 (&acc)[QM][QN]) {
 #pragma unroll
   for (int a = 0; a < QM; ++a)
@@ -1105,12 +1147,37 @@ __device__ __forceinline__ void acc4_store_t(double* Ct, size_t ld, const d4 (&a
   }
 }
 
+// 64 x 16 column-quarter stores (C layout of mma_64x16, quarter columns 16w..): C[r + c ld] =
+// sgn acc, C -= acc, and the transposed Ct[c + r ld] through the wave's [16][65] LDS buffer (four
+// 128-B row segments per store instruction)
+__device__ __forceinline__ void accq_store(double* C, size_t ld, const d4 (&acc)[QM], double sgn) {
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+#pragma unroll
+  for (int a = 0; a < QM; ++a)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) C[(size_t)(lk + 4 * q) * ld + 16 * a + lr] = sgn * acc[a][q];
+}
+__device__ __forceinline__ void accq_store_t(double* Ct, size_t ld, const d4 (&acc)[QM], double sgn, double* tb) {
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+#pragma unroll
+  for (int a = 0; a < QM; ++a)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) tb[(lk + 4 * q) * (TS + 1) + 16 * a + lr] = sgn * acc[a][q];  // tb[c][r]
+  __builtin_amdgcn_wave_barrier();
+  const int c = l & 15, r4 = l >> 4;
+#pragma unroll
+  for (int r = 0; r < TS; r += 4) Ct[(size_t)(r + r4) * ld + c] = tb[c * (TS + 1) + r + r4];
+  __builtin_amdgcn_wave_barrier();
+}
+
 __device__ __forceinline__ void leaf_body(const DevBatch& db, int o, int n) {
-  // one 64 x 64 tile task per wave (4 at a time); tile stores through the wave's LDS buffer
+  // every 64 x 64 tile task is split into four 64 x 16 column quarters, one per wave (wave w:
+  // columns 16w..16w+15 of every tile of a step), so a step with fewer tiles than waves keeps
+  // all four SIMDs busy; quarter-transposed stores through the wave's LDS buffer
   __shared__ double tbs[4 * 16 * (TS + 1)];
   const int slot = blockIdx.x;
   if (!slot_active(db, slot)) return;
-  const int w = threadIdx.x >> 6;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), cq = 16 * w;
   double* tb = tbs + w * 16 * (TS + 1);
   const size_t ld = db.ld, so = (size_t)slot * db.mat;
   double* K = db.K + so;
@@ -1122,50 +1189,48 @@ __device__ __forceinline__ void leaf_body(const DevBatch& db, int o, int n) {
     const int tk = o + k, m = n - 1 - k;
     diag_tile_fast(db, slot, tk);
     __syncthreads();
-    for (int t = w; t < m; t += 4) {  // TRSM: L[ti,tk] = K[ti,tk] Linv[tk,tk]^T
+    for (int t = 0; t < m; ++t) {  // TRSM: L[ti,tk] = K[ti,tk] Linv[tk,tk]^T
       const int ti = tk + 1 + t;
-      d4 acc[QM][QN];
-      acc4_zero(acc);
-      mma_64x64(acc, K + (size_t)tk * TS * ld + ti * TS, ld, Li + (size_t)tk * TS * ld + tk * TS, ld, TS);
-      acc4_store(Lw + (size_t)(tk * TS) * ld + ti * TS, ld, acc, 1.0);
+      d4 acc[QM];
+#pragma unroll
+      for (int a = 0; a < QM; ++a) acc[a] = (d4){0.0, 0.0, 0.0, 0.0};
+      mma_64x16(acc, K + (size_t)tk * TS * ld + ti * TS, ld, Li + (size_t)tk * TS * ld + tk * TS + cq, ld, TS);
+      accq_store(Lw + (size_t)(tk * TS + cq) * ld + ti * TS, ld, acc, 1.0);
     }
     __syncthreads();
-    for (int t = w; t < m * (m + 1) / 2; t += 4) {  // SYRK (lower trailing tiles)
-      int a = t, c = 0;
-      while (a >= m - c) {
-        a -= m - c;
-        ++c;
+    for (int c = 0; c < m; ++c)  // SYRK (lower trailing tiles)
+      for (int a0 = 0; a0 < m - c; ++a0) {
+        const int tj = tk + 1 + c, ti = tj + a0;
+        double* Ct = K + (size_t)(tj * TS + cq) * ld + ti * TS;
+        d4 acc[QM];  // -C - L L^T, stored negated
+#pragma unroll
+        for (int a = 0; a < QM; ++a)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc[a][q] = -Ct[(size_t)(lk + 4 * q) * ld + 16 * a + lr];
+        mma_64x16(acc, Lw + (size_t)tk * TS * ld + ti * TS, ld, Lw + (size_t)tk * TS * ld + tj * TS + cq, ld, TS);
+        accq_store(Ct, ld, acc, -1.0);
       }
-      const int tj = tk + 1 + c, ti = tj + a;
-      double* Ct = K + (size_t)(tj * TS) * ld + ti * TS;
-      d4 acc[QM][QN];  // -C - L L^T, stored negated
-#pragma unroll
-      for (int aa = 0; aa < QM; ++aa)
-#pragma unroll
-        for (int b = 0; b < QN; ++b)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) acc[aa][b][q] = -Ct[(size_t)(16 * b + lk + 4 * q) * ld + 16 * aa + lr];
-      mma_64x64(acc, Lw + (size_t)tk * TS * ld + ti * TS, ld, Lw + (size_t)tk * TS * ld + tj * TS, ld, TS);
-      acc4_store(Ct, ld, acc, -1.0);
-    }
     __syncthreads();
   }
   // off-diagonal inverse tiles by sub-diagonal s:  X = sum_{k=tj}^{ti-1} L[ti,k] Linv[k,tj] (kept
-  // transposed in Mt[tj,ti] as scratch), Linv[ti,tj] = -Linv[ti,ti] X; one wave per tile
+  // transposed in Mt[tj,ti] as scratch), Linv[ti,tj] = -Linv[ti,ti] X.  Wave w's quarter of
+  // Linv[ti,tj] needs only its own quarter of X: no barrier between the two products.
   for (int s = 1; s < n; ++s) {
-    for (int t = w; t < n - s; t += 4) {
+    for (int t = 0; t < n - s; ++t) {
       const int tj = o + t, ti = tj + s;
       double* Xt = Mt + (size_t)(ti * TS) * ld + tj * TS;  // Mt[tj,ti]
-      d4 acc[QM][QN];
-      acc4_zero(acc);
-      mma_64x64(acc, Lw + (size_t)tj * TS * ld + ti * TS, ld, Mt + (size_t)tj * TS * ld + tj * TS, ld, s * TS);
-      acc4_store_t(Xt, ld, acc, 1.0, tb);
+      d4 acc[QM];
+#pragma unroll
+      for (int a = 0; a < QM; ++a) acc[a] = (d4){0.0, 0.0, 0.0, 0.0};
+      mma_64x16(acc, Lw + (size_t)tj * TS * ld + ti * TS, ld, Mt + (size_t)tj * TS * ld + tj * TS + cq, ld, s * TS);
+      accq_store_t(Xt + cq, ld, acc, 1.0, tb);
       __threadfence_block();
-      acc4_zero(acc);
-      mma_64x64(acc, Li + (size_t)ti * TS * ld + ti * TS, ld, Xt, ld, TS);
+#pragma unroll
+      for (int a = 0; a < QM; ++a) acc[a] = (d4){0.0, 0.0, 0.0, 0.0};
+      mma_64x16(acc, Li + (size_t)ti * TS * ld + ti * TS, ld, Xt + cq, ld, TS);
       __threadfence_block();  // all lanes' reads of X precede the overwrite below
-      acc4_store(Li + (size_t)(tj * TS) * ld + ti * TS, ld, acc, -1.0);
-      acc4_store_t(Xt, ld, acc, -1.0, tb);
+      accq_store(Li + (size_t)(tj * TS + cq) * ld + ti * TS, ld, acc, -1.0);
+      accq_store_t(Xt + cq, ld, acc, -1.0, tb);
     }
     __syncthreads();
   }
