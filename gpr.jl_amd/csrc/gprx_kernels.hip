@@ -1235,31 +1235,37 @@ __device__ __forceinline__ void leaf_body(const DevBatch& db, int o, int n) {
     __syncthreads();
   }
   // z partials of the off-diagonal L^-1 tiles of this leaf, read back from L2 (this workgroup
-  // wrote them; the diagonal tiles' partials come from diag_tile_fast); <= 6 tiles, one barrier
+  // wrote them; the diagonal tiles' partials come from diag_tile_fast); 16 tiles per round (the
+  // [4][16][65] buffer), one round for leaves of <= 6 off-diagonal tiles
   __threadfence_block();
   {
     const int r = threadIdx.x & 63, qc = threadIdx.x >> 6;  // 4 quarters of 16 columns
-    int k = 0;
-    for (int s = 1; s < n; ++s)
-      for (int t = 0; t < n - s; ++t, ++k) {
-        const int tj = o + t, ti = tj + s;
-        const double* Lt = Li + (size_t)(tj * TS) * ld + ti * TS;
-        const double* y = db.Y + (size_t)slot * db.Npad + tj * TS;
-        double acc = 0.0;
-#pragma unroll
-        for (int c = 16 * qc; c < 16 * qc + 16; ++c) acc = fma(Lt[(size_t)c * ld + r], y[c], acc);
-        tbs[(4 * k + qc) * TS + r] = acc;  // k < 16: fits the [4][16][65] buffer
-      }
-    __syncthreads();
-    k = 0;
-    for (int s = 1; s < n; ++s)
-      for (int t = 0; t < n - s; ++t, ++k)
-        if (qc == 0) {
+    const int nod = n * (n - 1) / 2;
+    for (int k0 = 0; k0 < nod; k0 += 16) {
+      int k = 0;
+      for (int s = 1; s < n; ++s)
+        for (int t = 0; t < n - s; ++t, ++k) {
+          if (k < k0 || k >= k0 + 16) continue;
           const int tj = o + t, ti = tj + s;
-          const double* pk = tbs + 4 * k * TS;
-          zp_row(db, slot, 2 * tj)[ti * TS + r] = ((pk[r] + pk[TS + r]) + pk[2 * TS + r]) + pk[3 * TS + r];
-          zp_row(db, slot, 2 * tj + 1)[ti * TS + r] = 0.0;
+          const double* Lt = Li + (size_t)(tj * TS) * ld + ti * TS;
+          const double* y = db.Y + (size_t)slot * db.Npad + tj * TS;
+          double acc = 0.0;
+#pragma unroll
+          for (int c = 16 * qc; c < 16 * qc + 16; ++c) acc = fma(Lt[(size_t)c * ld + r], y[c], acc);
+          tbs[(4 * (k - k0) + qc) * TS + r] = acc;
         }
+      __syncthreads();
+      k = 0;
+      for (int s = 1; s < n; ++s)
+        for (int t = 0; t < n - s; ++t, ++k)
+          if (qc == 0 && k >= k0 && k < k0 + 16) {
+            const int tj = o + t, ti = tj + s;
+            const double* pk = tbs + 4 * (k - k0) * TS;
+            zp_row(db, slot, 2 * tj)[ti * TS + r] = ((pk[r] + pk[TS + r]) + pk[2 * TS + r]) + pk[3 * TS + r];
+            zp_row(db, slot, 2 * tj + 1)[ti * TS + r] = 0.0;
+          }
+      __syncthreads();
+    }
   }
 }
 

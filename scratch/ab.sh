@@ -9,6 +9,6 @@ for i in 1 2; do
     python -c "
 import json,sys
 for l in open('gpurun_out/ab_$v$i.log'):
-    if l.startswith('{'): d=json.loads(l); k=d['kernels_ms_per_step']; print('$v$i', d['ms_per_step'], 'lauum', k['lauum_grad'], 'leaf', k['leaf'], 'trsm', k['potrf_trsm'], 'syrk', k['syrk_tt'], 'linv', k['trtri_linv21'], 'alpha', k['alpha'], 'pv', k['pred_var'], flush=True)"
+    if l.startswith('{'): d=json.loads(l); k=d['kernels_ms_per_step']; print('$v$i', d['ms_per_step'], 'lauum', k['lauum_grad'], 'leaf', k['leaf'], 'trsm', k['potrf_trsm'], 'syrk', k['syrk_tt'], 'linv', k['trtri_linv21'], 'alpha', k['alpha'], 'pv', k['pred_var'], 'gram', k['gram'], flush=True)"
   done
 done

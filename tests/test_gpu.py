@@ -329,8 +329,8 @@ def test_graph_replay_matches_direct_launches(gprx, golden_dir):
 def test_factorisation_paths_match_golden(gprx, golden_dir, leaf, small_n):
     """Every recursion leaf (fused k_leaf for 2..8 tiles, the standalone 64x64 diagonal kernel at
     leaf 1) and both GEMM unit shapes (64 x 32 pair units below small_n tiles, 64 x 64 above)
-    give the golden results, at N=256 (4 tiles) and N=130 (ragged), and report the same failing
-    pivot on a non-PD slot."""
+    give the golden results at N=256 (4 tiles), the oracle's at N=130 (ragged) and N=512 (an
+    8-tile leaf at leaf 8), and report the same failing pivot on a non-PD slot."""
     c = gprx.Context(0)
     c.set_option(gprx.OPT_LEAF_TILES, leaf)
     c.set_option(gprx.OPT_SMALL_N, small_n)
@@ -357,6 +357,18 @@ def test_factorisation_paths_match_golden(gprx, golden_dir, leaf, small_n):
         b.set_test(Xs[:, :9])
         r = b.run(th[None], grad=True, predict=True)
         check_slot(r, 0, Xr, yr, th, Xs[:, :9], c.dist_mode)
+        b.close()
+        # N = 512: 8 tiles, one fused leaf of 28 off-diagonal tiles at leaf 8 (two rounds of the
+        # leaf's z-partial buffer)
+        from gprx import data
+
+        tr = data.make_trial("P2", 512, 9, seed=data.trial_seed("P2", 3))
+        th5 = data.theta0("P2", 512)
+        b = gprx.GPBatch(1, tr["X"].shape[0], 512, 9, ctx=c)
+        b.set_train(tr["X"], tr["Y"][:1])
+        b.set_test(tr["Xs"])
+        r = b.run(th5[None], grad=True, predict=True)
+        check_slot(r, 0, tr["X"], tr["Y"][0], th5, tr["Xs"], c.dist_mode)
         b.close()
         zn = np.load(golden_dir / "nonpd_p1.npz")
         b = gprx.GPBatch(1, zn["X"].shape[0], zn["X"].shape[1], 0, ctx=c)
