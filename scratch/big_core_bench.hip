@@ -72,8 +72,35 @@ __device__ __forceinline__ void core_sb(d4 (&acc)[WM][WN], const double* A, size
   }
 }
 
+
+// R register stages of depth 4 SD in a ring: stage it + R - 1 is loaded while stage it runs
+template <int WM, int WN, int SD, int R>
+__device__ __forceinline__ void core_ring(d4 (&acc)[WM][WN], const double* A, size_t lda, const double* B, size_t ldb, int K) {
+  const int nst = __builtin_amdgcn_readfirstlane(K / (4 * SD));
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  const double* pa = A + lr + (size_t)lk * lda;
+  const double* pb = B + lr + (size_t)lk * ldb;
+  const size_t sa = 4 * lda, sb = 4 * ldb;
+  Frag<WM, WN, SD> f[R];
+#pragma unroll
+  for (int r = 0; r < R - 1; ++r) {
+    const int n = r < nst ? r : nst - 1;
+    fload(f[r], pa + (size_t)n * SD * sa, pb + (size_t)n * SD * sb, sa, sb);
+  }
+  for (int it = 0; it < nst; it += R) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int nx = it + r + R - 1, n = nx < nst ? nx : nst - 1;
+      fload(f[(r + R - 1) % R], pa + (size_t)n * SD * sa, pb + (size_t)n * SD * sb, sa, sb);
+      __builtin_amdgcn_sched_barrier(0);
+      if (it + r < nst) fmma(acc, f[r]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
 // WG = 4 waves (2 x 2), wave tile (16 WM) x (16 WN); WG tile (32 WM) x (32 WN).
-template <int WM, int WN, int SD, bool SB = false>
+template <int WM, int WN, int SD, bool SB = false, int R = 0>
 __device__ __forceinline__ void body(const double* P, double* C, int T, int nbr, int K, int S) {
   const int x = blockIdx.x & 7, q = blockIdx.x >> 3;
   const int slot = (q / T) * 8 + x, u = q % T;
@@ -87,7 +114,8 @@ __device__ __forceinline__ void body(const double* P, double* C, int T, int nbr,
 #pragma unroll
     for (int b = 0; b < WN; ++b) acc[a][b] = (d4){0, 0, 0, 0};
   const int r0 = 1024 + bi * 32 * WM + 16 * WM * wr, c0 = bj * 32 * WN + 16 * WN * wc;
-  if constexpr (SB) core_sb<WM, WN, SD>(acc, M + r0, 2048, M + c0, 2048, K);
+  if constexpr (R > 0) core_ring<WM, WN, SD, R>(acc, M + r0, 2048, M + c0, 2048, K);
+  else if constexpr (SB) core_sb<WM, WN, SD>(acc, M + r0, 2048, M + c0, 2048, K);
   else core<WM, WN, SD>(acc, M + r0, 2048, M + c0, 2048, K);
   double* Cs = C + (size_t)slot * 1024 * 1024;
   const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
@@ -113,6 +141,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const double* P, double* C, int T, int nbr, int K, int S) {
   body<4, 4, 2, true>(P, C, T, nbr, K, S);
 }
+#define RING(NAME, SD, R)                                                                             \
+  __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void NAME(             \
+      const double* P, double* C, int T, int nbr, int K, int S) {                                     \
+    body<4, 4, SD, false, R>(P, C, T, nbr, K, S);                                                     \
+  }
+RING(k_ring_sd2_r3, 2, 3)
+RING(k_ring_sd1_r4, 1, 4)
+RING(k_ring_sd1_r3, 1, 3)
+RING(k_ring_sd2_r2, 2, 2)
 KERN(k_128x64_sd2_o2, 8, 4, 2, 2)
 KERN(k_128x64_sd4_o1, 8, 4, 4, 1)
 KERN(k_128x128_sd2_o1, 8, 8, 2, 1)
@@ -133,11 +170,13 @@ int main() {
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
   struct V { const char* name; const void* f; int WM, WN; };
-  V vs[] = {{"64x64 sd4 o2 (library)", (const void*)k_64x64_sd4_o2, 4, 4},
-            {"64x64 sd4 o2 sched-barrier", (const void*)k_64x64_sb_o2, 4, 4},
-            {"64x64 sd2 o2 sched-barrier", (const void*)k_64x64_sb2_o2, 4, 4},
-            {"128x64 sd4 o1", (const void*)k_128x64_sd4_o1, 8, 4}};
-  for (int K : {1024, 512, 256}) {
+  V vs[] = {{"64x64 sd4 o2 (no barriers)", (const void*)k_64x64_sd4_o2, 4, 4},
+            {"64x64 sd2 o2 sb (library)", (const void*)k_64x64_sb2_o2, 4, 4},
+            {"ring sd2 r2", (const void*)k_ring_sd2_r2, 4, 4},
+            {"ring sd2 r3", (const void*)k_ring_sd2_r3, 4, 4},
+            {"ring sd1 r4", (const void*)k_ring_sd1_r4, 4, 4},
+            {"ring sd1 r3", (const void*)k_ring_sd1_r3, 4, 4}};
+  for (int K : {1024, 512, 256, 128}) {
     bool first = true;
     for (auto& v : vs) {
       const int nbr = 1024 / (32 * v.WM), nbc = 1024 / (32 * v.WN), T = nbr * nbc;
