@@ -326,7 +326,7 @@ int run_eval(gprx_batch* b, bool want_grad, bool want_pred, bool factor) {
 
 // Per-call launch geometry from the context options and the batch size.
 void set_geometry(const gprx_ctx* c, DevBatch& db) {
-  db.small_n = c->small_n > 0 ? c->small_n : (db.B >= 32 ? 8 : 64);  // small batches: more, smaller units
+  db.small_n = c->small_n > 0 ? c->small_n : (db.B >= 32 ? 4 : 64);  // small batches: more, smaller units
 }
 
 }  // namespace

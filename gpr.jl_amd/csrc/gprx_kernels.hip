@@ -128,25 +128,27 @@ __device__ __forceinline__ void sqrt_rsqrt(double p, double& s, double& r) {
   s = p * r;
   s = fma(0.5 * r, fma(-s, s, p), s);
 }
-// exp(x) for x <= 0, relative error < 1e-14 (degree-11 Taylor on |r| <= ln2/2 after the
-// Cody-Waite reduction x = n ln2 + r): 17 instructions, no range checks beyond underflow.  Used
-// only for the gradient's recomputed Kf (tolerance 1e-7); K itself uses the library exp.
-__device__ __forceinline__ double exp_neg(double x) {
-  const double n = rint(x * 1.4426950408889634);
-  double r = fma(-n, 6.93147180369123816490e-01, x);
-  r = fma(-n, 1.90821492927058770002e-10, r);
-  double p = 2.505210838544172e-08;  // 1/11!
-  p = fma(p, r, 2.755731922398589e-07);
-  p = fma(p, r, 2.7557319223985893e-06);
-  p = fma(p, r, 2.48015873015873e-05);
-  p = fma(p, r, 1.984126984126984e-04);
-  p = fma(p, r, 1.388888888888889e-03);
-  p = fma(p, r, 8.333333333333333e-03);
-  p = fma(p, r, 4.1666666666666664e-02);
-  p = fma(p, r, 1.6666666666666666e-01);
-  p = fma(p, r, 0.5);
-  p = fma(p, r, 1.0);
-  p = fma(p, r, 1.0);
+// exp(x) for x <= 0 (the Gram's K and the gradient's recomputed Kf): Cody-Waite reduction
+// x = n ln2 + r (|r| <= ln2/2, r exact by fma), degree-13 Taylor polynomial (truncation
+// |r|^14/14! < 5e-18 relative, so about 1 ulp from the Horner rounding), ldexp; 0 below -745.
+// The coefficients live in a mutable device array that a kernel copies into registers once
+// (uniform loads: SGPRs): with literal constants the compiler rematerialises every coefficient
+// per exp as two v_mov_b32 (14 per exp: 897 extra VALU instructions per gradient tile).
+struct ExpK {
+  double c[14];  // 1/13!, 1/12!, ..., 1/2, 1, 1
+  double l2e, ln2hi, ln2lo;
+};
+__device__ ExpK g_expk = {{1.6059043836821613e-10, 2.08767569878681e-09, 2.505210838544172e-08, 2.755731922398589e-07,
+                           2.7557319223985893e-06, 2.48015873015873e-05, 0.0001984126984126984, 0.001388888888888889,
+                           0.008333333333333333, 0.041666666666666664, 0.16666666666666666, 0.5, 1.0, 1.0},
+                          1.4426950408889634, 6.93147180369123816490e-01, 1.90821492927058770002e-10};
+__device__ __forceinline__ double exp_k(double x, const ExpK& k) {
+  const double n = rint(x * k.l2e);
+  double r = fma(-n, k.ln2hi, x);
+  r = fma(-n, k.ln2lo, r);
+  double p = k.c[0];
+#pragma unroll
+  for (int i = 1; i < 14; ++i) p = fma(p, r, k.c[i]);
   return x < -745.0 ? 0.0 : ldexp(p, (int)n);
 }
 // 1/p by v_rcp_f64 + two Newton steps (|error| <= 1 ulp; the reference's dpotf2 scales by 1/ajj too)
@@ -167,6 +169,23 @@ __device__ __forceinline__ double readlane_d(double v, int lane) {
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+// v from another lane of the same 16-lane row by a DPP control (two 32-bit DPP moves, no LDS)
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const long long b = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, true);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+// sum over the 16 lanes of each row, the same value in every lane of the row: quad pairs (quad_perm
+// [1,0,3,2], [2,3,0,1]), then quad with quad (row_half_mirror), half-row with half-row (row_mirror)
+__device__ __forceinline__ double row_sum16(double v) {
+  v += dpp_f64<0xB1>(v);
+  v += dpp_f64<0x4E>(v);
+  v += dpp_f64<0x141>(v);
+  v += dpp_f64<0x140>(v);
   return v;
 }
 
@@ -482,6 +501,7 @@ __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
   for (int e = tid; e < d + 3; e += NTHR) pw[e] = P[e];
   __syncthreads();
   const double sf2 = pw[d], noise = pw[d + 1];
+  const ExpK ek = g_expk;
   const int rb = tid & 15, cb = tid >> 4;
   double rr[4][4];
 #pragma unroll
@@ -525,7 +545,7 @@ __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
       if (gi >= db.N || gj >= db.N) {
         kv[a] = (gi == gj) ? 1.0 : 0.0;
       } else {
-        const double fv = sf2 * exp(-rr[a][b] * 0.5);
+        const double fv = sf2 * exp_k(-rr[a][b] * 0.5, ek);
         kv[a] = (gi == gj) ? fv + noise : fv;
       }
     }
@@ -1288,18 +1308,35 @@ __global__ __launch_bounds__(NTHR) void k_alpha(DevBatch db, int phase) {
     return;
   }
   const size_t ld = db.ld;
-  const double* A = db.Mt + (size_t)slot * db.mat + i * TS + r;
+  // lane: rows 2 rp, 2 rp + 1 of the tile row (one 16-B load), columns of parity cp: one load
+  // instruction reads two whole 512-B column segments.  The column range [k0, Npad) is split in 4
+  // contiguous quarters of whole 16-column groups (wave-uniform, so z comes in by scalar loads).
+  const int rp = r & 31, cp = r >> 5, w = __builtin_amdgcn_readfirstlane(pt);
+  const double* A = db.Mt + (size_t)slot * db.mat + i * TS + 2 * rp + (size_t)cp * ld;
   const double* v = db.z + (size_t)slot * db.Npad;
   const int k0 = i * TS, k1 = db.Npad;
-  // columns [k0, k1) split in 4 contiguous quarters of whole 16-column groups, 8 loads in flight
-  const int ng = (k1 - k0) / 16, g0 = (ng * pt) / 4, g1 = (ng * (pt + 1)) / 4;
-  double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int ng = (k1 - k0) / 16, g0 = (ng * w) / 4, g1 = (ng * (w + 1)) / 4;
+  typedef double d2 __attribute__((ext_vector_type(2)));
+  d2 acc[4] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};
   for (int gq = g0; gq < g1; ++gq) {
     const int kk = k0 + 16 * gq;
+    d2 m[8];
 #pragma unroll
-    for (int u = 0; u < 16; ++u) acc[u & 7] = fma(A[(size_t)(kk + u) * ld], v[kk + u], acc[u & 7]);
+    for (int u = 0; u < 8; ++u) m[u] = *(const d2*)(A + (size_t)(kk + 2 * u) * ld);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const double zv = cp ? v[kk + 2 * u + 1] : v[kk + 2 * u];
+      acc[u & 3].x = fma(m[u].x, zv, acc[u & 3].x);
+      acc[u & 3].y = fma(m[u].y, zv, acc[u & 3].y);
+    }
   }
-  part[pt][r] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  double s0 = (acc[0].x + acc[1].x) + (acc[2].x + acc[3].x), s1 = (acc[0].y + acc[1].y) + (acc[2].y + acc[3].y);
+  s0 += __shfl_xor(s0, 32);  // the other column parity
+  s1 += __shfl_xor(s1, 32);
+  if (cp == 0) {
+    part[pt][2 * rp] = s0;
+    part[pt][2 * rp + 1] = s1;
+  }
   __syncthreads();
   if (pt == 0) {
     const double s = ((part[0][r] + part[1][r]) + part[2][r]) + part[3][r];
@@ -1412,6 +1449,7 @@ __device__ __forceinline__ void lauum_unit(const DevBatch& db, int slot, const i
     const double* ar = als + ir * TS;
     const double* ac = als + ic * TS;
     const int KS = (d + 3) >> 2;
+    const ExpK ek = g_expk;
     // G in place of acc:  Kf recomputed from r = n_r + n_c - 2 sum_p il2_p xc_pr xc_pc (MFMA, one
     // 16 x 16 block at a time; the same centred points as the distance sums below)
 #pragma unroll
@@ -1449,7 +1487,7 @@ __device__ __forceinline__ void lauum_unit(const DevBatch& db, int slot, const i
               tr += W;
             } else {
               const double rr = fma(-2.0, cr[q], nr[r] + nc[c]);
-              const double kf = sf2 * exp_neg(-0.5 * (rr > 0.0 ? rr : 0.0));
+              const double kf = sf2 * exp_k(-0.5 * (rr > 0.0 ? rr : 0.0), ek);
               G = W * kf;
             }
             sf += G;
@@ -1476,12 +1514,7 @@ __device__ __forceinline__ void lauum_unit(const DevBatch& db, int slot, const i
     for (int b = 0; b < QN; ++b)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        double s = (acc[0][b][q] + acc[1][b][q]) + (acc[2][b][q] + acc[3][b][q]);
-        s += __shfl_xor(s, 1);
-        s += __shfl_xor(s, 2);
-        s += __shfl_xor(s, 4);
-        s += __shfl_xor(s, 8);
-        Cs[b][q] = s;
+        Cs[b][q] = row_sum16((acc[0][b][q] + acc[1][b][q]) + (acc[2][b][q] + acc[3][b][q]));
       }
     const int H = (d + 15) >> 4;
 #pragma unroll 1
@@ -1515,14 +1548,7 @@ __device__ __forceinline__ void lauum_unit(const DevBatch& db, int slot, const i
         }
       }
 #pragma unroll
-      for (int qq = 0; qq < 4; ++qq) {
-        double s = t13[qq];
-        s += __shfl_xor(s, 1);
-        s += __shfl_xor(s, 2);
-        s += __shfl_xor(s, 4);
-        s += __shfl_xor(s, 8);
-        t13[qq] = s;
-      }
+      for (int qq = 0; qq < 4; ++qq) t13[qq] = row_sum16(t13[qq]);
       t2 += __shfl_xor(t2, 16);
       t2 += __shfl_xor(t2, 32);
       if (lr == 0) {

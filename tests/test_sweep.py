@@ -177,7 +177,9 @@ def test_fb_hyperparameter_optimise_n4096(ctx):
     b.set_train(X, Y)
     start = b.run(th0, grad=False)
     res, rounds = b.optimize(th0, LBFGS(), Options(max_evals=30), refit=True)
-    assert rounds <= 31
+    # max_evals is Optim's soft f_calls_limit (checked after each iteration: the last line search
+    # may overrun it); a round is at most one f call of each running slot
+    assert rounds <= max(x.f_calls for x in res)
     thmin = np.stack([x.minimizer for x in res])
     r = b.run(thmin, grad=False)
     for s in range(G):
