@@ -20,3 +20,5 @@ for c in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "SQ_INSTS_VALU_MFM
   echo "pmc $c done"
 done
 python3 profiles/summarize.py $OUT $R
+# the summaries land in the box's profiles/; copy them back with the run's other outputs
+cp profiles/${R}_summary.json profiles/pmc_latest.json $OUT/
