@@ -467,13 +467,18 @@ __device__ __forceinline__ void acc_zero(d4 (&acc)[WM][WN]) {
 // Gram: lower tiles of K (noise on the diagonal).  grid = B * ntl, 256 threads, each thread
 // a 4x4 register block; X tiles in dynamic LDS as [p][64].
 // ============================================================================================
+// Coordinate images in LDS, dimension-major with row stride CS = 66 doubles: the tile loads write
+// them with the dimension as the fast index across lanes, and a stride of 64 put every dimension of
+// a point in one bank (26-way conflicts on each ds_write_b64); 66 spreads them over the banks and
+// keeps the 16-B alignment of the inner loop's ds_read_b128.
+constexpr int CS = TS + 2;
 template <int MODE>
 __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int d = db.d, tid = threadIdx.x;
   double* xi = sm;
-  double* xj = sm + d * TS;
-  double* pw = sm + 2 * d * TS;
+  double* xj = sm + d * CS;
+  double* pw = sm + 2 * d * CS;
   int slot, t, i = 0, j = 0;
   if (!map_slot(db, db.ntl, slot, t)) return;
   {  // t-th lower tile in column-major order
@@ -495,8 +500,8 @@ __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
   for (int e = tid; e < TS * d; e += NTHR) {
     const int r = e / d, p = e - r * d;
     const double s = MODE == 1 ? sc[p] : 1.0;
-    xi[p * TS + r] = X[(size_t)i * TS * d + e] * s;
-    xj[p * TS + r] = X[(size_t)j * TS * d + e] * s;
+    xi[p * CS + r] = X[(size_t)i * TS * d + e] * s;
+    xj[p * CS + r] = X[(size_t)j * TS * d + e] * s;
   }
   for (int e = tid; e < d + 3; e += NTHR) pw[e] = P[e];
   __syncthreads();
@@ -509,10 +514,10 @@ __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
 #pragma unroll
     for (int b = 0; b < 4; ++b) rr[a][b] = 0.0;
   for (int p = 0; p < d; ++p) {
-    const double2 u0 = *(const double2*)(xi + p * TS + 4 * rb);
-    const double2 u1 = *(const double2*)(xi + p * TS + 4 * rb + 2);
-    const double2 v0 = *(const double2*)(xj + p * TS + 4 * cb);
-    const double2 v1 = *(const double2*)(xj + p * TS + 4 * cb + 2);
+    const double2 u0 = *(const double2*)(xi + p * CS + 4 * rb);
+    const double2 u1 = *(const double2*)(xi + p * CS + 4 * rb + 2);
+    const double2 v0 = *(const double2*)(xj + p * CS + 4 * cb);
+    const double2 v1 = *(const double2*)(xj + p * CS + 4 * cb + 2);
     const double av[4] = {u0.x, u0.y, u1.x, u1.y};
     const double bv[4] = {v0.x, v0.y, v1.x, v1.y};
     const double w = pw[p];
@@ -1711,8 +1716,8 @@ __global__ __launch_bounds__(NTHR) void k_pred_cross(DevBatch db) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int d = db.d, tid = threadIdx.x;
   double* xt = sm;
-  double* xs = sm + d * TS;
-  double* pw = sm + 2 * d * TS;
+  double* xs = sm + d * CS;
+  double* pw = sm + 2 * d * CS;
   int slot, t;
   if (!map_slot(db, db.nt * db.mt, slot, t)) return;
   const int ch = t / db.mt, mtile = t - ch * db.mt;
@@ -1727,8 +1732,8 @@ __global__ __launch_bounds__(NTHR) void k_pred_cross(DevBatch db) {
   for (int e = tid; e < TS * d; e += NTHR) {
     const int r = e / d, p = e - r * d;
     const double s = MODE == 1 ? sc[p] : 1.0;
-    xt[p * TS + r] = X[(size_t)ch * TS * d + e] * s;
-    xs[p * TS + r] = Xq[(size_t)mtile * TS * d + e] * s;
+    xt[p * CS + r] = X[(size_t)ch * TS * d + e] * s;
+    xs[p * CS + r] = Xq[(size_t)mtile * TS * d + e] * s;
   }
   for (int e = tid; e < d + 3; e += NTHR) pw[e] = P[e];
   __syncthreads();
@@ -1741,10 +1746,10 @@ __global__ __launch_bounds__(NTHR) void k_pred_cross(DevBatch db) {
 #pragma unroll
     for (int b = 0; b < 4; ++b) rr[a][b] = 0.0;
   for (int p = 0; p < d; ++p) {
-    const double2 u0 = *(const double2*)(xt + p * TS + 4 * rb);
-    const double2 u1 = *(const double2*)(xt + p * TS + 4 * rb + 2);
-    const double2 v0 = *(const double2*)(xs + p * TS + 4 * mb);
-    const double2 v1 = *(const double2*)(xs + p * TS + 4 * mb + 2);
+    const double2 u0 = *(const double2*)(xt + p * CS + 4 * rb);
+    const double2 u1 = *(const double2*)(xt + p * CS + 4 * rb + 2);
+    const double2 v0 = *(const double2*)(xs + p * CS + 4 * mb);
+    const double2 v1 = *(const double2*)(xs + p * CS + 4 * mb + 2);
     const double av[4] = {u0.x, u0.y, u1.x, u1.y};
     const double bv[4] = {v0.x, v0.y, v1.x, v1.y};
     const double wgt = pw[p];
@@ -1927,9 +1932,9 @@ __global__ __launch_bounds__(NT) void k_rollout(RolloutArgs a) {
 // ---------------------------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------------------------
-static size_t gram_lds(int d) { return (size_t)(2 * d * TS + 2 * DMAX + 4) * sizeof(double); }
+static size_t gram_lds(int d) { return (size_t)(2 * d * CS + 2 * DMAX + 4) * sizeof(double); }
 static size_t lauum_lds(const DevBatch& b) { return lauum_lds_dbl(b.xs, b.nimg) * sizeof(double); }
-static size_t cross_lds(int d) { return (size_t)(2 * d * TS + 2 * DMAX + 4) * sizeof(double); }
+static size_t cross_lds(int d) { return (size_t)(2 * d * CS + 2 * DMAX + 4) * sizeof(double); }
 
 static void set_lds_limits() {
   static bool done = false;
