@@ -287,12 +287,15 @@ __device__ __forceinline__ void mma_64x32_s1(d4 (&acc)[WM][WN], const double* __
 // 64 x 64 wave core (k_gemm, k_lauum_grad): acc[a][b] += A(64 x K) B(64 x K)^T, same operand and
 // C maps as mma_64x32 (acc[a][b] lane l reg q = C[16a + (l&15)][16b + (l>>4) + 4q]), 16 MFMAs
 // per 8 fragment loads, two register stages of depth 8 (Q4SD = 2 MFMA sub-steps) in ping-pong,
-// ~210 VGPRs: two waves per SIMD.  Scheduling barriers pin the four phases (load stage it+1, MFMA
-// stage it, load stage it+2, MFMA stage it+1): without them the compiler sinks the prefetch next
-// to the other stage's loads and waits on vmcnt(0) before the first MFMA, serialising load and
-// compute.  Measured on MI355X (scratch/big_core_bench.hip, 192 batched 1024 x 1024 panels,
-// 2 waves/SIMD): 70.9 / 68.5 / 64.2 TF/s at K = 1024 / 512 / 256, against 64.5 / 67.4 / 63.0 for
-// depth-16 stages without the barriers (and 60.2 / 57.4 / 52.7 for depth 16 with them: 25 spills).
+// ~210 VGPRs: two waves per SIMD.  Scheduling barriers pin the two halves of an iteration (stage
+// it+1's loads with stage it's MFMAs, stage it+2's loads with stage it+1's MFMAs): without them the
+// compiler sinks the prefetch next to the other stage's loads and waits on vmcnt(0) before the
+// first MFMA, serialising load and compute.  Inside a half, group barriers interleave one load per
+// two MFMAs (round 2: every GEMM 2-3% faster than with the loads issued as one burst before the
+// MFMAs, step 43.25 -> 42.7 ms at B=240, same-box A/B).  Measured on MI355X before the interleave
+// (scratch/big_core_bench.hip, 192 batched 1024 x 1024 panels, 2 waves/SIMD): 70.9 / 68.5 / 64.2
+// TF/s at K = 1024 / 512 / 256, against 64.5 / 67.4 / 63.0 for depth-16 stages without the
+// barriers (and 60.2 / 57.4 / 52.7 for depth 16 with them: 25 spills).
 // ---------------------------------------------------------------------------------------------
 constexpr int QM = 4, QN = 4, Q4SD = 2;
 struct Frag4 {
@@ -330,20 +333,30 @@ __device__ __forceinline__ void mma_64x64(d4 (&acc)[QM][QN], const double* __res
   Frag4 f0, f1;
   frag4_load<NB>(f0, pa, pb, sa, sb);
   for (int it = 0; it < nst; it += 2) {
-    frag4_load<NB>(f1, pa + (size_t)(it + 1) * Q4SD * sa, pb + (size_t)(it + 1) * Q4SD * sb, sa, sb);
     __builtin_amdgcn_sched_barrier(0);
+    frag4_load<NB>(f1, pa + (size_t)(it + 1) * Q4SD * sa, pb + (size_t)(it + 1) * Q4SD * sb, sa, sb);
     frag4_mma<NB>(acc, f0);
+#pragma unroll
+    for (int g = 0; g < Q4SD * (QM + NB); ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // one VMEM read
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // two MFMAs
+    }
     __builtin_amdgcn_sched_barrier(0);
     const int n2 = (it + 2 < nst) ? it + 2 : nst - 1;
     frag4_load<NB>(f0, pa + (size_t)n2 * Q4SD * sa, pb + (size_t)n2 * Q4SD * sb, sa, sb);
-    __builtin_amdgcn_sched_barrier(0);
     frag4_mma<NB>(acc, f1);
+#pragma unroll
+    for (int g = 0; g < Q4SD * (QM + NB); ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+    }
     __builtin_amdgcn_sched_barrier(0);
   }
 }
 // 64 x 16 wave core (the fused leaf's column-quarter tasks): acc[a] += A(64 x K) B(16 x K)^T,
 // lane l reg q = C[16a + (l&15)][(l>>4) + 4q]; 4 MFMAs per 5 fragment loads, stages of depth 16
-// in ping-pong (the same phase barriers as mma_64x64).  K: whole 64-tiles.
+// in ping-pong (the same barriers as mma_64x64, groups of 5 loads and 4 MFMAs interleaved: leaf
+// 2.18 -> 2.09 ms at B=240, same-box A/B).  K: whole 64-tiles.
 struct Frag16 {
   double a[4][QM], b[4];
 };
@@ -372,14 +385,23 @@ __device__ __forceinline__ void mma_64x16(d4 (&acc)[QM], const double* __restric
   Frag16 f0, f1;
   frag16_load(f0, pa, pb, sa, sb);
   for (int it = 0; it < nst; it += 2) {
-    frag16_load(f1, pa + (size_t)(it + 1) * 4 * sa, pb + (size_t)(it + 1) * 4 * sb, sa, sb);
     __builtin_amdgcn_sched_barrier(0);
+    frag16_load(f1, pa + (size_t)(it + 1) * 4 * sa, pb + (size_t)(it + 1) * 4 * sb, sa, sb);
     frag16_mma(acc, f0);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x020, 5, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+    }
     __builtin_amdgcn_sched_barrier(0);
     const int n2 = (it + 2 < nst) ? it + 2 : nst - 1;
     frag16_load(f0, pa + (size_t)n2 * 4 * sa, pb + (size_t)n2 * 4 * sb, sa, sb);
-    __builtin_amdgcn_sched_barrier(0);
     frag16_mma(acc, f1);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x020, 5, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+    }
     __builtin_amdgcn_sched_barrier(0);
   }
 }
