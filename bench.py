@@ -82,7 +82,7 @@ def pmc_traffic(stat: str, global_batch: int):
         if (s.get("bench_under_rocprof") or {}).get("config", {}).get("global_batch") != global_batch:
             return None
         for k, e in s["kernels"].items():
-            if k.startswith(sym) and "traffic_bytes_per_launch" in e:
+            if k.split()[-1].startswith(sym) and "traffic_bytes_per_launch" in e:  # "void k_gram<1>"
                 return {"bytes_per_launch": e["traffic_bytes_per_launch"], "source": f"profiles/{s['round']}_summary.json",
                         "kernel_symbol": k}
     except Exception:
