@@ -405,6 +405,28 @@ __device__ __forceinline__ void mma_64x16(d4 (&acc)[QM], const double* __restric
     __builtin_amdgcn_sched_barrier(0);
   }
 }
+// mma_64x16 with the B operand from the wave's LDS buffer: B(j, k) = tb[j * (TS + 1) + k] (a
+// column quarter kept transposed in LDS by the producer), K = 64 (one tile)
+__device__ __forceinline__ void mma_64x16_ldsb(d4 (&acc)[QM], const double* __restrict__ A, size_t lda, const double* tb) {
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  const double* pa = A + lr + (size_t)lk * lda;
+  const double* pb = tb + lr * (TS + 1) + lk;
+  const size_t sa = 4 * lda;
+#pragma unroll
+  for (int st = 0; st < TS / 16; ++st) {
+    double a[4][QM], b[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+#pragma unroll
+      for (int q = 0; q < QM; ++q) a[s][q] = pa[(size_t)(4 * st + s) * sa + 16 * q];
+      b[s] = pb[16 * st + 4 * s];
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int q = 0; q < QM; ++q) acc[q] = mfma(b[s], a[s][q], acc[q]);
+  }
+}
 __device__ __forceinline__ void acc4_zero(d4 (&acc)[QM][QN]) {
 #pragma unroll
   for (int a = 0; a < QM; ++a)
@@ -1130,7 +1152,7 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
 // most) in ONE workgroup per slot, replacing ~4n latency-bound launches of the recursion.
 //   for k: diag(o+k); Lw[i,k] = K[i,k] Linv[k,k]^T (i > k); K[i,j] -= Lw[i,k] Lw[j,k]^T (i >= j > k)
 //   then the off-diagonal inverse tiles by sub-diagonal s = i - j:
-//     X = sum_{t=j}^{i-1} L[i,t] Linv[t,j]  (into Mt[j,i] as scratch),  Linv[i,j] = -Linv[i,i] X
+//     X = sum_{t=j}^{i-1} L[i,t] Linv[t,j]  (per wave quarter, in LDS),  Linv[i,j] = -Linv[i,i] X
 // Each 64x64 tile task runs on a wave pair (columns 32*half..+31), two tasks at a time.  The X of
 // a task is only re-read by the wave that wrote it (its own 32 columns), so a wave-level fence
 // replaces a barrier between the two products.
@@ -1260,7 +1282,7 @@ __device__ __forceinline__ void leaf_body(const DevBatch& db, int o, int n) {
     __syncthreads();
   }
   // off-diagonal inverse tiles by sub-diagonal s:  X = sum_{k=tj}^{ti-1} L[ti,k] Linv[k,tj] (kept
-  // transposed in Mt[tj,ti] as scratch), Linv[ti,tj] = -Linv[ti,ti] X.  Wave w's quarter of
+  // transposed in the wave's LDS buffer), Linv[ti,tj] = -Linv[ti,ti] X.  Wave w's quarter of
   // Linv[ti,tj] needs only its own quarter of X: no barrier between the two products.
   for (int s = 1; s < n; ++s) {
     for (int t = 0; t < n - s; ++t) {
@@ -1270,12 +1292,17 @@ __device__ __forceinline__ void leaf_body(const DevBatch& db, int o, int n) {
 #pragma unroll
       for (int a = 0; a < QM; ++a) acc[a] = (d4){0.0, 0.0, 0.0, 0.0};
       mma_64x16(acc, Lw + (size_t)tj * TS * ld + ti * TS, ld, Mt + (size_t)tj * TS * ld + tj * TS + cq, ld, s * TS);
-      accq_store_t(Xt + cq, ld, acc, 1.0, tb);
-      __threadfence_block();
+      // this wave's quarter of X stays in its LDS buffer, transposed (tb[c][r] = X[r][cq + c]):
+      // the second product reads it from there instead of a global round trip
+#pragma unroll
+      for (int a = 0; a < QM; ++a)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) tb[(lk + 4 * q) * (TS + 1) + 16 * a + lr] = acc[a][q];
+      __builtin_amdgcn_wave_barrier();
 #pragma unroll
       for (int a = 0; a < QM; ++a) acc[a] = (d4){0.0, 0.0, 0.0, 0.0};
-      mma_64x16(acc, Li + (size_t)ti * TS * ld + ti * TS, ld, Xt + cq, ld, TS);
-      __threadfence_block();  // all lanes' reads of X precede the overwrite below
+      mma_64x16_ldsb(acc, Li + (size_t)ti * TS * ld + ti * TS, ld, tb);
+      __builtin_amdgcn_wave_barrier();  // the reads of X precede accq_store_t's writes to tb
       accq_store(Li + (size_t)(tj * TS + cq) * ld + ti * TS, ld, acc, -1.0);
       accq_store_t(Xt + cq, ld, acc, -1.0, tb);
     }
