@@ -646,12 +646,13 @@ __global__ __launch_bounds__(NTHR) void k_center(DevBatch db) {
 // 16x16x4 f64 MFMA operand maps (gfx950): A lane l = A[l&15][l>>4], B lane l = B[l>>4][l&15],
 // D lane l reg q = D[(l>>4) + 4q][l&15].
 // ============================================================================================
-__device__ __forceinline__ void diag_tile_fast(const DevBatch& db, int slot, int jt);
+__device__ __forceinline__ void diag_tile_fast(const DevBatch& db, int slot, int jt, const double** xi_out = nullptr);
 __global__ __launch_bounds__(NTHR) void k_diag_f(DevBatch db, int jt) {
   if (slot_active(db, blockIdx.x)) diag_tile_fast(db, blockIdx.x, jt);
 }
 constexpr int FS = TS + 1;  // LDS column stride of the tile images
-__device__ __forceinline__ void diag_tile_fast(const DevBatch& db, int slot, int jt) {
+// xi_out: the LDS image of the tile's inverse (Xi[c * FS + r] = L^-1[r][c]), valid until the next call
+__device__ __forceinline__ void diag_tile_fast(const DevBatch& db, int slot, int jt, const double** xi_out) {
   __shared__ double T[TS * FS];   // T[c*FS + r] = A[r][c], then L (lower)
   __shared__ double Xi[TS * FS];  // Xi[c*FS + r] = X[r][c] = (L^-1)[r][c]
   __shared__ __attribute__((aligned(16))) double cbs[256];
@@ -822,6 +823,7 @@ __device__ __forceinline__ void diag_tile_fast(const DevBatch& db, int slot, int
     Mj[(size_t)c * ld + r] = (c >= r) ? Xi[r * FS + c] : 0.0;  // Mt[r][c] = X[c][r]
   }
   zp_diag(db, slot, jt, Xi, 1, FS, cbs);
+  if (xi_out) *xi_out = Xi;
 }
 
 
@@ -1256,14 +1258,15 @@ __device__ __forceinline__ void leaf_body(const DevBatch& db, int o, int n) {
   const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
   for (int k = 0; k < n; ++k) {
     const int tk = o + k, m = n - 1 - k;
-    diag_tile_fast(db, slot, tk);
+    const double* xi;  // Linv[tk,tk] in LDS, read by the TRSM tasks below
+    diag_tile_fast(db, slot, tk, &xi);
     __syncthreads();
     for (int t = 0; t < m; ++t) {  // TRSM: L[ti,tk] = K[ti,tk] Linv[tk,tk]^T
       const int ti = tk + 1 + t;
       d4 acc[QM];
 #pragma unroll
       for (int a = 0; a < QM; ++a) acc[a] = (d4){0.0, 0.0, 0.0, 0.0};
-      mma_64x16(acc, K + (size_t)tk * TS * ld + ti * TS, ld, Li + (size_t)tk * TS * ld + tk * TS + cq, ld, TS);
+      mma_64x16(acc, K + (size_t)tk * TS * ld + ti * TS, ld, xi + cq, FS, TS);
       accq_store(Lw + (size_t)(tk * TS + cq) * ld + ti * TS, ld, acc, 1.0);
     }
     __syncthreads();
