@@ -1246,6 +1246,7 @@ __device__ __forceinline__ void leaf_body(const DevBatch& db, int o, int n) {
   // columns 16w..16w+15 of every tile of a step), so a step with fewer tiles than waves keeps
   // all four SIMDs busy; quarter-transposed stores through the wave's LDS buffer
   __shared__ double tbs[4 * 16 * (TS + 1)];
+  __shared__ double zq[6][4][TS];  // n <= 4: z partials of the off-diagonal L^-1 quarters [tile][wave][row]
   const int slot = blockIdx.x;
   if (!slot_active(db, slot)) return;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), cq = 16 * w;
@@ -1287,8 +1288,9 @@ __device__ __forceinline__ void leaf_body(const DevBatch& db, int o, int n) {
   // off-diagonal inverse tiles by sub-diagonal s:  X = sum_{k=tj}^{ti-1} L[ti,k] Linv[k,tj] (kept
   // transposed in the wave's LDS buffer), Linv[ti,tj] = -Linv[ti,ti] X.  Wave w's quarter of
   // Linv[ti,tj] needs only its own quarter of X: no barrier between the two products.
+  int kz = 0;  // off-diagonal tile index in (s, t) order
   for (int s = 1; s < n; ++s) {
-    for (int t = 0; t < n - s; ++t) {
+    for (int t = 0; t < n - s; ++t, ++kz) {
       const int tj = o + t, ti = tj + s;
       double* Xt = Mt + (size_t)(ti * TS) * ld + tj * TS;  // Mt[tj,ti]
       d4 acc[QM];
@@ -1306,14 +1308,44 @@ __device__ __forceinline__ void leaf_body(const DevBatch& db, int o, int n) {
       for (int a = 0; a < QM; ++a) acc[a] = (d4){0.0, 0.0, 0.0, 0.0};
       mma_64x16_ldsb(acc, Li + (size_t)ti * TS * ld + ti * TS, ld, tb);
       __builtin_amdgcn_wave_barrier();  // the reads of X precede accq_store_t's writes to tb
+      if (n <= 4) {  // this quarter's z partial, from the registers: sum_c Linv[r][cq + c] y[cq + c]
+        const double* yq = db.Y + (size_t)slot * db.Npad + tj * TS + cq;
+        double yv[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) yv[q] = yq[lk + 4 * q];
+#pragma unroll
+        for (int a = 0; a < QM; ++a) {
+          double zt = 0.0;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) zt = fma(-acc[a][q], yv[q], zt);
+          zt += __shfl_xor(zt, 16);
+          zt += __shfl_xor(zt, 32);
+          if (lk == 0) zq[kz][w][16 * a + lr] = zt;
+        }
+      }
       accq_store(Li + (size_t)(tj * TS + cq) * ld + ti * TS, ld, acc, -1.0);
       accq_store_t(Xt + cq, ld, acc, -1.0, tb);
     }
     __syncthreads();
   }
-  // z partials of the off-diagonal L^-1 tiles of this leaf, read back from L2 (this workgroup
-  // wrote them; the diagonal tiles' partials come from diag_tile_fast); 16 tiles per round (the
-  // [4][16][65] buffer), one round for leaves of <= 6 off-diagonal tiles
+  // z partials of the off-diagonal L^-1 tiles of this leaf (the diagonal tiles' come from
+  // diag_tile_fast).  n <= 4: the four quarters' partials from zq, summed in wave order.
+  if (n <= 4) {
+    const int r = threadIdx.x & 63;
+    for (int k = threadIdx.x >> 6; k < n * (n - 1) / 2; k += 4) {
+      int s = 1, t = k;
+      while (t >= n - s) {
+        t -= n - s;
+        ++s;
+      }
+      const int tj = o + t, ti = tj + s;
+      zp_row(db, slot, 2 * tj)[ti * TS + r] = ((zq[k][0][r] + zq[k][1][r]) + zq[k][2][r]) + zq[k][3][r];
+      zp_row(db, slot, 2 * tj + 1)[ti * TS + r] = 0.0;
+    }
+    return;
+  }
+  // larger leaves: read the tiles back from L2 (this workgroup wrote them); 16 tiles per round
+  // (the [4][16][65] buffer)
   __threadfence_block();
   {
     const int r = threadIdx.x & 63, qc = threadIdx.x >> 6;  // 4 quarters of 16 columns
