@@ -646,22 +646,25 @@ __global__ __launch_bounds__(NTHR) void k_center(DevBatch db) {
 // 16x16x4 f64 MFMA operand maps (gfx950): A lane l = A[l&15][l>>4], B lane l = B[l>>4][l&15],
 // D lane l reg q = D[(l>>4) + 4q][l&15].
 // ============================================================================================
-__device__ __forceinline__ void diag_tile_fast(const DevBatch& db, int slot, int jt, const double** xi_out = nullptr);
-__global__ __launch_bounds__(NTHR) void k_diag_f(DevBatch db, int jt) {
-  if (slot_active(db, blockIdx.x)) diag_tile_fast(db, blockIdx.x, jt);
-}
 constexpr int FS = TS + 1;  // LDS column stride of the tile images
-// xi_out: the LDS image of the tile's inverse (Xi[c * FS + r] = L^-1[r][c]), valid until the next call
-__device__ __forceinline__ void diag_tile_fast(const DevBatch& db, int slot, int jt, const double** xi_out) {
-  __shared__ double T[TS * FS];   // T[c*FS + r] = A[r][c], then L (lower)
-  __shared__ double Xi[TS * FS];  // Xi[c*FS + r] = X[r][c] = (L^-1)[r][c]
+// LDS of the diagonal routine (the caller's): T[c*FS + r] = A[r][c], then L (lower); Xi[c*FS + r]
+// = X[r][c] = (L^-1)[r][c] (the inverse stays there until the next call); cbs: [256] scratch.
+// t_ready: T already holds the tile's lower triangle (zeros above), written by the caller.
+__device__ __forceinline__ void diag_tile_fast(const DevBatch& db, int slot, int jt, double* T, double* Xi, double* cbs,
+                                               bool t_ready);
+__global__ __launch_bounds__(NTHR) void k_diag_f(DevBatch db, int jt) {
+  __shared__ double T[TS * FS], Xi[TS * FS];
   __shared__ __attribute__((aligned(16))) double cbs[256];
+  if (slot_active(db, blockIdx.x)) diag_tile_fast(db, blockIdx.x, jt, T, Xi, cbs, false);
+}
+__device__ __forceinline__ void diag_tile_fast(const DevBatch& db, int slot, int jt, double* T, double* Xi, double* cbs,
+                                               bool t_ready) {
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, lr = l & 15, lk = l >> 4;
   const size_t ld = db.ld;
   const double* A = db.K + (size_t)slot * db.mat + (size_t)jt * TS * ld + jt * TS;
   for (int e = tid; e < TS * TS; e += NTHR) {
     const int r = e & 63, c = e >> 6;
-    T[c * FS + r] = (r >= c) ? A[(size_t)c * ld + r] : 0.0;
+    if (!t_ready) T[c * FS + r] = (r >= c) ? A[(size_t)c * ld + r] : 0.0;
     Xi[c * FS + r] = 0.0;
   }
   __syncthreads();
@@ -823,7 +826,6 @@ __device__ __forceinline__ void diag_tile_fast(const DevBatch& db, int slot, int
     Mj[(size_t)c * ld + r] = (c >= r) ? Xi[r * FS + c] : 0.0;  // Mt[r][c] = X[c][r]
   }
   zp_diag(db, slot, jt, Xi, 1, FS, cbs);
-  if (xi_out) *xi_out = Xi;
 }
 
 
@@ -1247,6 +1249,8 @@ __device__ __forceinline__ void leaf_body(const DevBatch& db, int o, int n) {
   // all four SIMDs busy; quarter-transposed stores through the wave's LDS buffer
   __shared__ double tbs[4 * 16 * (TS + 1)];
   __shared__ double zq[6][4][TS];  // n <= 4: z partials of the off-diagonal L^-1 quarters [tile][wave][row]
+  __shared__ double dT[TS * FS], dXi[TS * FS];  // the diagonal routine's tile and inverse images
+  __shared__ __attribute__((aligned(16))) double dcb[256];
   const int slot = blockIdx.x;
   if (!slot_active(db, slot)) return;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), cq = 16 * w;
@@ -1259,8 +1263,8 @@ __device__ __forceinline__ void leaf_body(const DevBatch& db, int o, int n) {
   const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
   for (int k = 0; k < n; ++k) {
     const int tk = o + k, m = n - 1 - k;
-    const double* xi;  // Linv[tk,tk] in LDS, read by the TRSM tasks below
-    diag_tile_fast(db, slot, tk, &xi);
+    const double* xi = dXi;  // Linv[tk,tk] in LDS, read by the TRSM tasks below
+    diag_tile_fast(db, slot, tk, dT, dXi, dcb, k > 0);  // k > 0: the SYRK below left the tile in dT
     __syncthreads();
     for (int t = 0; t < m; ++t) {  // TRSM: L[ti,tk] = K[ti,tk] Linv[tk,tk]^T
       const int ti = tk + 1 + t;
@@ -1281,7 +1285,17 @@ __device__ __forceinline__ void leaf_body(const DevBatch& db, int o, int n) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) acc[a][q] = -Ct[(size_t)(lk + 4 * q) * ld + 16 * a + lr];
         mma_64x16(acc, Lw + (size_t)tk * TS * ld + ti * TS, ld, Lw + (size_t)tk * TS * ld + tj * TS + cq, ld, TS);
-        accq_store(Ct, ld, acc, -1.0);
+        if (c == 0 && a0 == 0) {  // the next diagonal tile: straight into the diagonal routine's LDS
+#pragma unroll
+          for (int a = 0; a < QM; ++a)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const int r = 16 * a + lr, cc = cq + lk + 4 * q;
+              dT[cc * FS + r] = r >= cc ? -acc[a][q] : 0.0;
+            }
+        } else {
+          accq_store(Ct, ld, acc, -1.0);
+        }
       }
     __syncthreads();
   }
