@@ -836,6 +836,7 @@ __device__ __forceinline__ void diag_tile_fast(const DevBatch& db, int slot, int
 // return at once (no workgroup barrier in this kernel).
 // ============================================================================================
 // One 64 x 64 output tile (ti, tj) of a GemmOp on one wave.
+constexpr int TT_S = TS + 2;  // row stride of k_gemm's per-wave transpose buffer (LINV21's Mt store)
 template <bool PV>
 __device__ __forceinline__ void gemm_tile(const DevBatch& db, const GemmGeom& g, int slot, int ti, int tj) {
   const int op = PV ? (int)OP_PREDVAR : g.op;
@@ -918,17 +919,19 @@ __device__ __forceinline__ void gemm_tile(const DevBatch& db, const GemmGeom& g,
   if (op == OP_LINV21) {  // Mt[tj, ti] = Linv[ti, tj]^T, transposed through LDS 16 rows at a time
     // so that every store instruction writes one contiguous 512-B column segment of Mt
     extern __shared__ __attribute__((aligned(16))) double gsm[];
-    double* tb = gsm + (threadIdx.x >> 6) * (16 * (TS + 1));  // this wave's [16][65] buffer
+    // this wave's [16][66] buffer: at row stride 66 the 16 x 4 lanes of a store write 64 distinct
+    // banks per half-wave (stride 65 put lanes with equal lr + lk in one bank)
+    double* tb = gsm + (threadIdx.x >> 6) * (16 * TT_S);
     double* Mtt = db.Mt + so + (size_t)(ti * TS) * ld + tj * TS;
 #pragma unroll
     for (int a = 0; a < QM; ++a) {
 #pragma unroll
       for (int b = 0; b < QN; ++b)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) tb[lr * (TS + 1) + 16 * b + lk + 4 * q] = -acc[a][b][q];
+        for (int q = 0; q < 4; ++q) tb[lr * TT_S + 16 * b + lk + 4 * q] = -acc[a][b][q];
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
-      for (int r = 0; r < 16; ++r) Mtt[(size_t)(16 * a + r) * ld + l] = tb[r * (TS + 1) + l];
+      for (int r = 0; r < 16; ++r) Mtt[(size_t)(16 * a + r) * ld + l] = tb[r * TT_S + l];
       __builtin_amdgcn_wave_barrier();
     }
   }
@@ -2071,7 +2074,7 @@ void launch_gemm(const DevBatch& b, const GemmGeom& g, hipStream_t s, const Gemm
   }
   int T = op_units(g, b.nt, b.mt);
   if (g2.op != OP_NONE) T += op_units(g2, b.nt, b.mt);
-  const size_t lds = (g.op == OP_LINV21 || g2.op == OP_LINV21) ? 4 * 16 * (TS + 1) * sizeof(double) : 0;
+  const size_t lds = (g.op == OP_LINV21 || g2.op == OP_LINV21) ? 4 * 16 * TT_S * sizeof(double) : 0;
   if (g.op == OP_PREDVAR) hipLaunchKernelGGL(k_gemm_pv, dim3(grid_blocks(b.B, T)), dim3(NTHR), lds, s, b, g, g2);
   else hipLaunchKernelGGL(k_gemm, dim3(grid_blocks(b.B, T)), dim3(NTHR), lds, s, b, g, g2);
 }
