@@ -1160,69 +1160,10 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
 //   for k: diag(o+k); Lw[i,k] = K[i,k] Linv[k,k]^T (i > k); K[i,j] -= Lw[i,k] Lw[j,k]^T (i >= j > k)
 //   then the off-diagonal inverse tiles by sub-diagonal s = i - j:
 //     X = sum_{t=j}^{i-1} L[i,t] Linv[t,j]  (per wave quarter, in LDS),  Linv[i,j] = -Linv[i,i] X
-// Each 64x64 tile task runs on a wave pair (columns 32*half..+31), two tasks at a time.  The X of
-// a task is only re-read by the wave that wrote it (its own 32 columns), so a wave-level fence
-// replaces a barrier between the two products.
+// Each 64x64 tile task is split into four 64x16 column quarters, one per wave.  The X of a task is
+// only re-read by the wave that computed it (its own 16 columns, kept in the wave's LDS buffer), so
+// a wave-level barrier replaces a workgroup barrier between the two products.
 // ============================================================================================
-__device__ __forceinline__ void acc_store(double* C, size_t ld, const d4 (&acc)[WM][WN], double sgn) {
-  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
-#pragma unroll
-  for (int a = 0; a < WM; ++a)
-#pragma unroll
-    for (int b = 0; b < WN; ++b)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) C[(size_t)(16 * b + lk + 4 * q) * ld + 16 * a + lr] = sgn * acc[a][b][q];
-}
-__device__ __forceinline__ void acc_sub(double* C, size_t ld, const d4 (&acc)[WM][WN]) {
-  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
-#pragma unroll
-  for (int a = 0; a < WM; ++a)
-#pragma unroll
-    for (int b = 0; b < WN; ++b)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        double* p = C + (size_t)(16 * b + lk + 4 * q) * ld + 16 * a + lr;
-        *p = *p - acc[a][b][q];
-      }
-}
-// transposed store: Ct[c][r] = sgn * C[r][c]  (Ct points at the transposed block's origin)
-__device__ __forceinline__ void acc_store_t(double* Ct, size_t ld, const d4 (&acc)[WM][WN], double sgn) {
-  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
-#pragma unroll
-  for (int a = 0; a < WM; ++a)
-#pragma unroll
-    for (int b = 0; b < WN; ++b)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) Ct[(size_t)(16 * a + lr) * ld + 16 * b + lk + 4 * q] = sgn * acc[a][b][q];
-}
-
-// 64 x 64 accumulator tile stores (C layout of mma_64x64): C[r + c ld] = sgn acc, and the
-// transposed Ct[c + r ld] = sgn acc through a per-wave [16][65] LDS buffer (contiguous 512-B
-// column segments instead of 16-way scattered rows).
-__device__ __forceinline__ void acc4_store(double* C, size_t ld, const d4 (&acc)[QM][QN], double sgn) {
-  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
-#pragma unroll
-  for (int a = 0; a < QM; ++a)
-#pragma unroll
-    for (int b = 0; b < QN; ++b)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) C[(size_t)(16 * b + lk + 4 * q) * ld + 16 * a + lr] = sgn * acc[a][b][q];
-}
-__device__ __forceinline__ void acc4_store_t(double* Ct, size_t ld, const d4 (&acc)[QM][QN], double sgn, double* tb) {
-  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
-#pragma unroll
-  for (int a = 0; a < QM; ++a) {
-#pragma unroll
-    for (int b = 0; b < QN; ++b)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) tb[lr * (TS + 1) + 16 * b + lk + 4 * q] = sgn * acc[a][b][q];
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int r = 0; r < 16; ++r) Ct[(size_t)(16 * a + r) * ld + l] = tb[r * (TS + 1) + l];
-    __builtin_amdgcn_wave_barrier();
-  }
-}
-
 // 64 x 16 column-quarter stores (C layout of mma_64x16, quarter columns 16w..): C[r + c ld] =
 // sgn acc, C -= acc, and the transposed Ct[c + r ld] through the wave's [16][65] LDS buffer (four
 // 128-B row segments per store instruction)
