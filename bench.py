@@ -8,8 +8,11 @@ One "step" = one batch of fits: T trials x 6 output GPs (vwindices of P2noise.jl
 each GP with its own theta (config.json P2_MAX2048 jittered, as during optimisation), inputs
 resident in HBM before the timed region.
 
-Launch: python bench.py [--gpus N --steps K --warmup W]; for N>1 under torch.distributed.run
-(one rank per GPU).  Trials are sharded over ranks by the product sharding module
+Launch: python bench.py [--gpus N --steps K --warmup W].  For N>1 the ranks run one per GPU over
+RCCL: under torch.distributed.run (the driver's form), or started by this script itself as a
+torch.distributed.run child when WORLD_SIZE is unset; fewer visible GPUs than N is an error
+(--rehearse lets ranks share devices with a gloo control plane, for rehearsals only), and every
+rank checks world size == N and the backend.  Trials are sharded over ranks by the product sharding module
 (gprx.shard: trial-major round robin, one RankBatch = one device batch of all the rank's trials x
 outputs per GPU; weak scaling, no data-path collective).  Rank 0 prints ONE JSON line.
 """
@@ -90,6 +93,24 @@ def pmc_traffic(stat: str, global_batch: int):
     return None
 
 
+def pmc_field(stat: str, global_batch: int, fields):
+    """Selected per-kernel fields of the committed PMC summary (same workload only), or None."""
+    f = REPO / "profiles" / "pmc_latest.json"
+    sym = SYMBOL.get(stat)
+    if sym is None or not f.exists():
+        return None
+    try:
+        s = json.loads(f.read_text())
+        if (s.get("bench_under_rocprof") or {}).get("config", {}).get("global_batch") != global_batch:
+            return None
+        for k, e in s["kernels"].items():
+            if k.split()[-1].startswith(sym):
+                return {q: e.get(q) for q in fields} | {"source": f"profiles/{s['round']}_summary.json"}
+    except Exception:
+        return None
+    return None
+
+
 def roofline_parts(kern: dict, nprof: int, global_batch: int) -> dict:
     """The north star's two roofline figures beside the dominant kernel's: the Gram build against
     HBM (algorithmic bytes 8 (Npad^2/2 + Npad d) per slot: the lower tiles of K written, X read)
@@ -118,18 +139,64 @@ def roofline_parts(kern: dict, nprof: int, global_batch: int) -> dict:
             d["traffic_source"] = tr
         return d
 
-    return {"gram": part(["gram"], "hbm"),
+    gram = part(["gram"], "hbm")
+    if gram is not None:
+        # the Gram is priced against HBM (the north star's figure) but HBM does not bind it: its
+        # PMC traffic is ~1.03x the algorithmic bytes and its VALU issue floor (SQ_INSTS_VALU x 4
+        # cycles / 1024 SIMDs at the PMC clock) is ~0.9 of its time: VALU(+LDS)-bound
+        gram["binding_limit"] = "valu"
+        gram["valu_floor"] = pmc_field("gram", global_batch, ("valu_floor_ms", "valu_floor_frac", "clock_ghz_est"))
+    return {"gram": gram,
             "factorisation": part(["leaf", "diag", "potrf_trsm", "syrk_tt", "trtri_linv21"], "mfma"),
             "lauum_grad": part(["lauum_grad"], "mfma"),
             "pred_var": part(["pred_var"], "mfma")}
 
 
+def _cgroup_cpus():
+    """The CPU quota of this process's cgroup: (raw text, CPUs as a float or None when unlimited /
+    unreadable).  cgroup v2 cpu.max ("quota period" or "max period"), else v1 cfs_quota_us /
+    cfs_period_us."""
+    cands = ["/sys/fs/cgroup/cpu.max"]
+    try:  # the process's own cgroup path (v2: "0::/path")
+        for line in pathlib.Path("/proc/self/cgroup").read_text().splitlines():
+            parts = line.split(":", 2)
+            if len(parts) == 3 and parts[0] == "0" and parts[2] not in ("", "/"):
+                cands.insert(0, f"/sys/fs/cgroup{parts[2]}/cpu.max")
+    except OSError:
+        pass
+    for p in cands:
+        try:
+            raw = pathlib.Path(p).read_text().strip()
+        except OSError:
+            continue
+        q, per = (raw.split() + ["100000"])[:2]
+        return f"{p}: {raw}", (None if q == "max" else int(q) / int(per))
+    for d in ("/sys/fs/cgroup/cpu", "/sys/fs/cgroup/cpu,cpuacct"):
+        try:
+            q = int(pathlib.Path(d, "cpu.cfs_quota_us").read_text())
+            per = int(pathlib.Path(d, "cpu.cfs_period_us").read_text())
+        except (OSError, ValueError):
+            continue
+        return f"{d}/cpu.cfs_quota_us: {q} / {per}", (None if q < 0 else q / per)
+    return "no cgroup cpu controller readable", None
+
+
 def _host_cores():
-    """(cores used, nproc): nproc = CPUs this process may run on (sched_getaffinity); the cores
-    used are the box's CPU share when the launcher states one (OMP_NUM_THREADS), else nproc."""
+    """The CPUs the box grants this process and how the baseline's thread count follows from them:
+    affinity (sched_getaffinity), the cgroup quota and OMP_NUM_THREADS are all read and reported.
+    cores = the affinity capped by the cgroup quota when one is set (the CPUs the kernel will
+    actually schedule us on); without a quota, the launcher's stated share (OMP_NUM_THREADS) caps
+    it; else the whole affinity set.  Returns (cores, facts dict)."""
     nproc = len(os.sched_getaffinity(0))
+    raw, quota = _cgroup_cpus()
     share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-    return (min(share, nproc) if share > 0 else nproc), nproc
+    if quota is not None:
+        cores, rule = max(1, min(nproc, int(quota))), "min(affinity, cgroup quota)"
+    elif share > 0:
+        cores, rule = min(share, nproc), "no cgroup quota: min(affinity, OMP_NUM_THREADS)"
+    else:
+        cores, rule = nproc, "no cgroup quota, no OMP_NUM_THREADS: affinity"
+    return cores, dict(affinity=nproc, cgroup=raw, cgroup_quota_cpus=quota, omp_num_threads=share or None, rule=rule)
 
 
 def _oracle_fit_worker(args):
@@ -166,7 +233,8 @@ def cpu_baseline(X, Y, T, XT, gpu=None, max_seconds: float = 15.0, max_fits: int
     from oracle import gp_oracle as O
     from threadpoolctl import threadpool_limits
 
-    cores, nproc = _host_cores()
+    cores, facts = _host_cores()
+    nproc = facts["affinity"]
     out = {}
     impl = "numpy"
     try:
@@ -225,12 +293,12 @@ def cpu_baseline(X, Y, T, XT, gpu=None, max_seconds: float = 15.0, max_fits: int
     best = max(out, key=lambda k: out[k]["value"])
     how = ("oracle/cpu_fit.c: C on the host's OpenBLAS (dpotrf/dpotrs/dtrsm), OpenMP threads for the trial-parallel "
            "mode" if impl == "c" else "oracle/gp_oracle.py: numpy + the host's OpenBLAS")
-    base = dict(value=out[best]["value"], unit="fits/s", cores=cores, kind="port", nproc=nproc, mode=best, modes=out,
-                impl=impl,
+    base = dict(value=out[best]["value"], unit="fits/s", cores=cores, kind="port", nproc=nproc, host_cpus=facts,
+                mode=best, modes=out, impl=impl,
                 sample=f"P2 fits (N=2048, d=26, M=100) of the bench workload via {how} (reference algorithm: "
                        f"KernelData distance stack, direct distances, dpotrf, K^-1 by dpotrs on I, per-parameter "
                        f"gradient sums), each mode bounded to ~{max_seconds:.0f} s; value = the faster mode ({best}); "
-                       f"{cores} of nproc={nproc} host CPUs used")
+                       f"{cores} of nproc={nproc} host CPUs used ({facts['rule']}; {facts['cgroup']})")
     acc = None
     if gpu is not None and n_err:
         acc = dict(err, slots=n_err, tolerance_mu_rel=1e-9, tolerance_mll_rel=1e-10, tolerance_grad_rel=1e-7,
@@ -242,6 +310,33 @@ def _progress(rank: int, msg: str):
     """One progress line on stderr (rank 0): the JSON result stays the only stdout line."""
     if rank == 0:
         print(f"bench: {msg}", file=sys.stderr, flush=True)
+
+
+def _launch_ranks(args) -> int:
+    """`bench.py --gpus N` (N > 1) started without a launcher: start N ranks, one per GPU, as a
+    torch.distributed.run child (the driver's own command line), and return its exit code.  Runs
+    before this process touches a GPU (device_count() does not initialise one on this image).  Too
+    few visible GPUs is an error, not a silent one-rank run; --rehearse lets ranks share devices."""
+    import socket
+
+    import torch
+
+    ndev = torch.cuda.device_count()
+    if ndev < args.gpus and not args.rehearse:
+        print(f"bench: --gpus {args.gpus} needs {args.gpus} visible GPUs, this host has {ndev} "
+              f"(--rehearse runs the ranks on shared devices, for a rehearsal only)", file=sys.stderr)
+        return 2
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), str(pathlib.Path(__file__).resolve()),
+           *sys.argv[1:]]
+    _progress(0, f"launching {args.gpus} ranks: {' '.join(cmd[1:6])} ...")
+    import subprocess
+
+    return subprocess.run(cmd).returncode
 
 
 def main():
@@ -257,25 +352,39 @@ def main():
     ap.add_argument("--no-prof", action="store_true")
     ap.add_argument("--no-opt", action="store_true")
     ap.add_argument("--opt-evals", type=int, default=30)
+    ap.add_argument("--rehearse", action="store_true",
+                    help="allow more ranks than visible GPUs (ranks share devices, gloo control plane): a "
+                         "rehearsal of the distributed path, never a measurement")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(_launch_ranks(args))  # parent: no GPU call has been made
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU "
+              f"(python bench.py --gpus N starts them itself)", file=sys.stderr)
+        sys.exit(2)
     import torch
 
     dist = None
     ndev = torch.cuda.device_count()
-    dev = local % max(1, ndev)  # rehearsal with more ranks than GPUs shares a device
+    if ndev < 1 or (world > ndev and not args.rehearse):
+        print(f"bench: {world} rank(s) need {world} GPUs, {ndev} visible", file=sys.stderr)
+        sys.exit(2)
+    dev = local % ndev  # only a --rehearse run puts two ranks on one device
     torch.cuda.set_device(dev)
-    backend = "nccl"
+    backend = None
     if world > 1:
         import torch.distributed as dist
 
-        # the collectives here are control plane only (barrier, max of the timings); RCCL when every
-        # rank has its own GPU, gloo for a shared-device rehearsal
-        backend = "nccl" if ndev >= world else "gloo"
+        # the collectives here are control plane only (barrier, max of the timings, the per-rank
+        # rates): RCCL over xGMI, one rank per GPU; gloo only for a shared-device --rehearse run
+        backend = "gloo" if args.rehearse else "nccl"
         dist.init_process_group(backend)
+        assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
+        assert dist.get_backend() == backend, dist.get_backend()
 
     import gprx
 
@@ -307,10 +416,16 @@ def main():
     dt = time.perf_counter() - t0
     ok = ok and bool(np.all(r["status"] == 0))
     r = {k: np.asarray(v).reshape((B,) + np.asarray(v).shape[2:]) for k, v in r.items()}  # per slot
+    per_rank = [B * args.steps / dt]
     if dist is not None:
-        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{dev}" if backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+        cdev = f"cuda:{dev}" if backend == "nccl" else "cpu"
+        t = torch.tensor([dt, B * args.steps / dt, float(ok)], dtype=torch.float64, device=cdev)
+        allt = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(allt, t)
+        allt = torch.stack(allt).cpu().numpy()
+        dt = float(allt[:, 0].max())  # the slowest rank's time
+        per_rank = [float(v) for v in allt[:, 1]]
+        ok = bool(np.all(allt[:, 2] == 1.0))
     fits = B * args.steps * world
     value = fits / dt
 
@@ -401,6 +516,9 @@ def main():
             "config": {"workload": f"P2 double pendulum: {args.trials} trials x {G} output GPs per GPU, N={N}, "
                                    f"d={d}, M={M} test points; fit = Gram+Cholesky+alpha+LML, full dLML, predict mean+var",
                        "global_batch": fits // args.steps, "N": N, "d": d, "M": M, "parallelism": f"trial-shard x{world}"},
+            "ranks": world,
+            "backend": backend or "single process",
+            "per_rank_fits_per_s": [round(v, 3) for v in per_rank],
             "fit_ok": ok,
             "whole_step_tflops": round(step_flops / (dt / args.steps) / 1e12 * 1.0, 3),
             "whole_step_frac_of_fp64_peak": round(step_flops / (dt / args.steps) / 1e12 / PEAK_FP64_TFLOPS, 4),

@@ -46,8 +46,8 @@ struct gprx_ctx {
   // recursion nodes of <= this many tiles run fused in k_leaf; 0 = auto: 4 for batches of >= 32
   // slots (fewer launches), 1 below that (GPRX_OPT_LEAF_TILES)
   int leaf_tiles = 0;
-  // recursion nodes of <= this many tiles use the 64 x 32 pair-unit GEMM; 0 = auto: 8 for batches
-  // of >= 32 slots, every node below that (GPRX_OPT_SMALL_N)
+  // recursion nodes of <= this many tiles use the 64 x 32 pair-unit GEMM; 0 = auto (set_geometry:
+  // 4 for batches of >= 32 slots, every node below that) (GPRX_OPT_SMALL_N)
   int small_n = 0;
   // replay each batch's launch sequence as a hipGraph (GPRX_OPT_GRAPHS).  Off by default: measured
   // equal to direct launches at B=1..192 (the launches are queued far ahead of the GPU).
@@ -334,6 +334,15 @@ void set_geometry(const gprx_ctx* c, DevBatch& db) {
 extern "C" {
 
 int gprx_abi_version(void) { return GPRX_ABI_VERSION; }
+
+int gprx_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return n;
+}
 
 const char* gprx_status_string(int s) {
   switch (s) {
@@ -671,6 +680,11 @@ int gprx_batch_alpha(gprx_batch* b, double* alpha) {
   HIPCHK(c, hipMemcpy2DAsync(alpha, (size_t)db.N * sizeof(double), db.alpha, (size_t)db.Npad * sizeof(double),
                              (size_t)db.N * sizeof(double), db.B, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  // h_status holds the per-slot status of the evaluation that factorised the batch (gprx_batch_run
+  // or the optimiser's refit): a slot that failed there has no alpha
+  for (int s = 0; s < db.B; ++s)
+    if (b->h_status[s] != GPRX_OK)
+      for (int t = 0; t < db.N; ++t) alpha[(size_t)s * db.N + t] = NAN;
   return GPRX_OK;
 }
 

@@ -26,8 +26,9 @@ struct DevBatch {
   int want_var;                // predictive variance requested (var output non-NULL); 0 skips the
                                // O(N^2 M) variance GEMM (predictdynamics.jl uses the mean only)
   int small_n;                 // recursion nodes of <= small_n tiles use the 64 x 32 pair-unit GEMM
-                               // (default 8 for B >= 32, all nodes below that, where the 64 x 64
-                               // units leave most of the chip idle); larger: 64 x 64 core
+                               // (default, set_geometry in gprx_api.hip: 4 for B >= 32, all nodes
+                               // below that, where the 64 x 64 units leave most of the chip idle);
+                               // larger: 64 x 64 core
   int xs;                      // row stride of Xc: d | 1 (odd: spreads LDS banks)
   int pst;                     // stride of params per slot
   int gps;                     // stride of per-unit gradient partials (d + 2)

@@ -161,7 +161,7 @@ __device__ void lbfgs_slot(const LbArgs& a, const DevBatch& db, int slot, int in
     I[I_PH] = I[I_RESUME];
   }
   const double iterfinitemax = 52.0;  // -log2(eps(Float64))
-  const bool capped = a.max_evals >= 0;
+  const bool capped = a.max_evals > 0;  // Optim: f_calls_limit > 0 && f_calls >= f_calls_limit
   // run until the slot needs an evaluation that is not its cached one, or finishes
   for (int guard = 0; guard < 4096; ++guard) {
     int ph = I[I_PH];

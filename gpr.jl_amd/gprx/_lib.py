@@ -53,6 +53,8 @@ _vp = C.c_void_p
 SIGNATURES = {
     "gprx_abi_version": (C.c_int, []),
     "gprx_status_string": (C.c_char_p, [C.c_int]),
+    "gprx_build_id": (C.c_char_p, []),
+    "gprx_device_count": (C.c_int, []),
     "gprx_ctx_create": (C.c_int, [C.c_int, C.POINTER(_vp)]),
     "gprx_ctx_destroy": (None, [_vp]),
     "gprx_ctx_last_error": (C.c_char_p, [_vp]),
@@ -108,7 +110,34 @@ def _load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    want = source_build_id()
+    got = lib.gprx_build_id().decode()
+    if want is not None and got != want:
+        raise ImportError(f"gprx: {LIB_PATH} was built from other sources (build id {got}, sources {want}): "
+                          "stale library -- rebuild with `make -C gpr.jl_amd` (or __graft_entry__.build())")
     return lib
+
+
+# the library's sources, in the order gpr.jl_amd/Makefile hashes them (SRC then HDR)
+BUILD_SOURCES = ["csrc/gprx_kernels.hip", "csrc/gprx_lbfgs.hip", "csrc/gprx_projection.hip", "csrc/gprx_api.hip",
+                 "csrc/gprx_internal.h", "../include/gprx.h"]
+
+
+def source_build_id():
+    """SHA-256 prefix of the sources next to the default library (None when the library comes from
+    elsewhere via GPRX_LIB, or the sources are not shipped)."""
+    import hashlib
+
+    if "GPRX_LIB" in os.environ:
+        return None
+    root = _HERE.parent
+    h = hashlib.sha256()
+    for f in BUILD_SOURCES:
+        p = root / f
+        if not p.exists():
+            return None
+        h.update(p.read_bytes())
+    return h.hexdigest()[:16]
 
 
 lib = _load()

@@ -90,6 +90,37 @@ def _f64(a):
     return np.ascontiguousarray(a, dtype=np.float64)
 
 
+def opt_options(method=None, options=None, refit: bool = True) -> "L.OptOptions":
+    """gprx_opt_options from gprx.optim.LBFGS / Options, validated here (ValueError) with the same
+    bounds gprx_batch_optimize enforces, so a rejected call never reaches the library."""
+    import math
+
+    from .optim import LBFGS, Options
+
+    method = method or LBFGS()
+    options = options or Options()
+    ls = method.linesearch
+    if ls.order != 2:
+        raise ValueError("device optimiser: BackTracking order 2 only (the experiments' setting)")
+    if not 1 <= int(method.m) <= 64:
+        raise ValueError(f"LBFGS m = {method.m}: the device optimiser keeps 1..64 history pairs")
+    if int(options.iterations) < 0 or int(ls.iterations) < 0 or int(options.successive_f_tol) < 0:
+        raise ValueError("iterations, linesearch iterations and successive_f_tol must be >= 0")
+    if not (ls.c_1 > 0 and ls.rho_lo > 0 and ls.rho_hi > 0) or not math.isfinite(method.alphaguess) \
+            or math.isnan(options.g_abstol):
+        raise ValueError("c_1, rho_lo, rho_hi > 0; finite alphaguess; g_abstol not NaN")
+    o = L.OptOptions()
+    L.lib.gprx_opt_defaults(C.byref(o))
+    o.m, o.iterations, o.ls_iterations = method.m, options.iterations, ls.iterations
+    o.scaleinvH0, o.refit = int(method.scaleinvH0), int(refit)
+    o.successive_f_tol = int(options.successive_f_tol)
+    o.max_evals = 0 if options.max_evals is None else int(options.max_evals)  # <= 0: no limit (Optim)
+    o.g_abstol, o.alphaguess = options.g_abstol, method.alphaguess
+    o.time_limit = options.time_limit  # NaN: none
+    o.c_1, o.rho_hi, o.rho_lo = ls.c_1, ls.rho_hi, ls.rho_lo
+    return o
+
+
 class GPBatch:
     """B exact SE-ARD GPs with shared (d, N); per-slot X, y, theta.
 
@@ -181,35 +212,23 @@ class GPBatch:
         factorised at the minimisers (optimize!'s update_target!), so predict() uses them.  A
         minimiser whose refit fails raises (update_target!'s PosDefException / ArgumentError) with
         the results attached as `err.results`; the batch is then left unfactorised."""
-        from .optim import LBFGS, Options, Result
+        from .optim import Result
 
-        method = method or LBFGS()
-        options = options or Options()
+        o = opt_options(method, options, refit)
         theta0 = _f64(theta0)
         if theta0.ndim == 1:
             theta0 = np.broadcast_to(theta0, (self.B, self.d + 2)).copy()
         assert theta0.shape == (self.B, self.d + 2), theta0.shape
-        ls = method.linesearch
-        if ls.order != 2:
-            raise ValueError("device optimiser: BackTracking order 2 only (the experiments' setting)")
-        o = L.OptOptions()
-        L.lib.gprx_opt_defaults(C.byref(o))
-        o.m, o.iterations, o.ls_iterations = method.m, options.iterations, ls.iterations
-        o.scaleinvH0, o.refit = int(method.scaleinvH0), int(refit)
-        o.successive_f_tol = int(options.successive_f_tol)
-        o.max_evals = -1 if options.max_evals is None else int(options.max_evals)
-        o.g_abstol, o.alphaguess = options.g_abstol, method.alphaguess
-        o.time_limit = options.time_limit  # NaN: none
-        o.c_1, o.rho_hi, o.rho_lo = ls.c_1, ls.rho_hi, ls.rho_lo
         B, n = self.B, self.d + 2
         th = np.empty((B, n))
         fmin = np.empty(B)
-        its, fc, gc, stp = (np.empty(B, dtype=np.int32) for _ in range(4))
+        its, fc, gc = (np.empty(B, dtype=np.int32) for _ in range(3))
+        stp = np.full(B, -1, dtype=np.int32)  # -1: not written (the call rejected its input)
         rounds = C.c_int(0)
         rc = L.lib.gprx_batch_optimize(self.h, L.dptr(theta0), C.byref(o), L.dptr(th), L.dptr(fmin), L.iptr(its),
                                        L.iptr(fc), L.iptr(gc), L.iptr(stp), C.byref(rounds))
-        if rc not in (L.OK, L.NOT_POSITIVE_DEFINITE, L.INVALID_ARGUMENT):
-            L.check(rc, self.ctx.h)
+        if rc not in (L.OK, L.NOT_POSITIVE_DEFINITE, L.INVALID_ARGUMENT) or np.any(stp < 0):
+            L.check(rc if rc != L.OK else L.DEVICE_ERROR, self.ctx.h)  # no search ran: no results
         res = [Result(th[s].copy(), float(fmin[s]), int(its[s]), int(fc[s]), int(gc[s]),
                       bool(stp[s] & L.STOP_CONVERGED), L.STOP_NAMES[int(stp[s]) & 0xFF]) for s in range(B)]
         if rc != L.OK:  # the refit at a minimiser failed: the search results are still valid
@@ -229,7 +248,8 @@ class GPBatch:
         return mu, var
 
     def alpha(self):
-        """alpha = K^-1 (y - mean) per slot from the last successful factorisation (gp.alpha)."""
+        """alpha = K^-1 (y - mean) per slot from the last factorisation (gp.alpha); NaN rows for the
+        slots that failed in it."""
         out = np.empty((self.B, self.N))
         L.check(L.lib.gprx_batch_alpha(self.h, L.dptr(out)), self.ctx.h)
         return out

@@ -137,7 +137,8 @@ class Options:
     g_abstol: float = 1e-8
     time_limit: float = math.nan
     successive_f_tol: int = 1
-    max_evals: int | None = None  # Optim's f_calls_limit: a soft limit on f calls
+    max_evals: int | None = None  # Optim's f_calls_limit: a soft limit on f calls;
+    # None or <= 0: no limit (Optim's f_calls_limit = 0 default)
 
 
 @dataclass
@@ -274,7 +275,8 @@ def lbfgs_steps(x0, method: LBFGS | None = None, options: Options | None = None)
         if not math.isnan(options.time_limit) and time.time() - t0 > options.time_limit:
             stopped = "time_limit"
             break
-        if options.max_evals is not None and calls["f"] >= options.max_evals:  # f_calls_limit
+        # Optim: f_limit_reached = f_calls_limit > 0 && f_calls >= f_calls_limit (0 / None: no limit)
+        if options.max_evals is not None and options.max_evals > 0 and calls["f"] >= options.max_evals:
             stopped = "max_evals"
             break
         if not np.all(np.isfinite(g)):

@@ -90,6 +90,10 @@ def run_group(mech: str, N: int, variant: str, trial_ids, ctx, testsamples: int 
     ok_gp = opt["status"] == 0  # (n, G)
     err = np.full(n, math.inf)
     perr = np.zeros(n)
+    # a trial whose experiment would throw in the reference (a failed refit: PosDefException /
+    # ArgumentError from update_target!; a singular projection: SingularException) is dropped by
+    # parallelrun (core.jl:41-53: result = nothing, resultcallback! throws, nothing is pushed)
+    failed = np.ones(n, dtype=bool)
     t1 = time.perf_counter()
     if variant == "max":
         # predictdynamics for every test CState of every good trial in one launch
@@ -107,7 +111,8 @@ def run_group(mech: str, N: int, variant: str, trial_ids, ctx, testsamples: int 
                     continue
                 truth = data.test_truth(mech, testsamples, trials[i]["seed"], simsteps)["X"].T
                 err[i] = data.position_mse(truth, fin[sl])
-                perr[i] = float(np.mean(pe[sl]))  # projectionerror / length(xtest_old) (P2noise.jl:51)
+                perr[i] = float(np.mean(pe[sl]))
+                failed[i] = False  # projectionerror / length(xtest_old) (P2noise.jl:51)
     else:
         usesin = variant == "min_sin"
         nc = NCOORD[mech]
@@ -122,8 +127,9 @@ def run_group(mech: str, N: int, variant: str, trial_ids, ctx, testsamples: int 
                 pred = np.stack([final_cstate(mech, row[0::2]) for row in f])
                 truth = data.test_truth(mech, testsamples, trials[i]["seed"], simsteps)["X"].T
                 err[i] = data.position_mse(truth, pred)
+                failed[i] = False
     t_eval = time.perf_counter() - t1
-    out = dict(kstep_mse=err, projectionerror=perr, mll=opt["mll"], theta=opt["theta"], status=opt["status"],
+    out = dict(kstep_mse=err, projectionerror=perr, failed=failed, mll=opt["mll"], theta=opt["theta"], status=opt["status"],
                f_calls=opt["f_calls"],
                rounds=opt["rounds"], t_opt=t_opt, t_eval=t_eval, slots=n * G)
     if keep:
@@ -153,21 +159,27 @@ def run(mechs=MECHS, sizes=SIZES, variants=VARIANTS, n_trials: int = 100, testsa
             for var in variants:
                 r = run_group(mech, N, var, mine, ctx, testsamples, simsteps, max_evals, time_limit)
                 local = {"kstep_mse": r.get("kstep_mse", np.zeros(0)), "perr": r.get("projectionerror", np.zeros(0)),
+                         "failed": r.get("failed", np.zeros(0, dtype=bool)).astype(np.float64),
                          "ok": np.all(r["status"] == 0, axis=1).astype(np.float64) if r else np.zeros(0),
                          "t": np.full(len(mine), r.get("t_opt", 0.0) + r.get("t_eval", 0.0))}
                 if dist:
                     g = shard.gather_results({k: v.reshape(-1, 1) for k, v in local.items()}, n_trials,
                                              lambda q: shard.shard_trials(n_trials, q, world), 0,
-                                             keys=("kstep_mse", "perr", "ok", "t"))
+                                             keys=("kstep_mse", "perr", "failed", "ok", "t"))
                 else:
                     g = {k: v.reshape(-1, 1) for k, v in local.items()}
                 key = f"{mech}_{'MAX' if var == 'max' else 'MIN'}{N}"
                 if rank == 0:
-                    ks = [None if not math.isfinite(float(v)) else float(v) for v in g["kstep_mse"][:, 0]]
+                    # failed trials are left out of both lists (core.jl:41-53), nprocessed counts them;
+                    # a non-finite error of a trial that ran (a diverged rollout) is kept as the
+                    # reference keeps it (written as JSON Infinity / NaN)
+                    keep = g["failed"][:, 0] == 0
                     et = ETYPE[var]
-                    results.setdefault(et, {})[key] = {"nprocessed": n_trials, "kstep_mse": ks,
-                                                       "projectionerror": [float(v) for v in g["perr"][:, 0]],
-                                                       "variant": var, "ok": int(g["ok"][:, 0].sum())}
+                    results.setdefault(et, {})[key] = {"nprocessed": n_trials,
+                                                       "kstep_mse": [float(v) for v in g["kstep_mse"][keep, 0]],
+                                                       "projectionerror": [float(v) for v in g["perr"][keep, 0]],
+                                                       "variant": var, "ok": int(g["ok"][:, 0].sum()),
+                                                       "dropped": int((~keep).sum())}
                     timing[f"{key}/{var}"] = {"seconds_max_rank": float(np.max(g["t"][:, 0])) if n_trials else 0.0,
                                               "gp_fits": n_trials * (len(data.VW_INDICES[mech]) if var == "max"
                                                                      else NCOORD[mech])}

@@ -26,14 +26,20 @@ using LinearAlgebra
 const LIB = joinpath(@__DIR__, "..", "lib", "libgprx.so")
 const OK, NOT_PD, INVALID = Cint(0), Cint(1), Cint(2)
 
-# one context (HIP stream) per Julia thread; device = thread mod #GPUs (core.jl:28 workers)
+# one context (HIP stream) per Julia thread; device = thread mod #GPUs (core.jl:28 workers), the
+# device count from the library (GPRX_NGPU, if set, caps it, e.g. to leave GPUs to other jobs)
 const CTX = Dict{Int,Ptr{Cvoid}}()
+function ndevices()
+    n = Int(ccall((:gprx_device_count, LIB), Cint, ()))
+    n > 0 || error("gprx: no visible GPU")
+    haskey(ENV, "GPRX_NGPU") ? clamp(parse(Int, ENV["GPRX_NGPU"]), 1, n) : n
+end
 const CTX_LOCK = ReentrantLock()
 function context()
     tid = Threads.threadid()
     lock(CTX_LOCK) do
         get!(CTX, tid) do
-            ngpu = parse(Int, get(ENV, "GPRX_NGPU", "1"))
+            ngpu = ndevices()
             h = Ref{Ptr{Cvoid}}(C_NULL)
             rc = ccall((:gprx_ctx_create, LIB), Cint, (Cint, Ref{Ptr{Cvoid}}), (tid - 1) % ngpu, h)
             rc == OK || error("gprx_ctx_create failed ($rc)")

@@ -73,6 +73,12 @@ typedef struct gprx_gp gprx_gp;
 
 int gprx_abi_version(void);
 const char* gprx_status_string(int status);
+/* first 16 hex digits of the SHA-256 of the sources the library was built from (the host checks
+ * it against the sources it ships with, so a stale prebuilt library is refused)                 */
+const char* gprx_build_id(void);
+/* number of visible devices (hipGetDeviceCount; 0 when none or on error): hosts map their worker
+ * threads / ranks onto devices with it (core.jl:28's threads, jobid mod ndevices)               */
+int gprx_device_count(void);
 
 /* ---- context: one device, one stream ------------------------------------------------------ */
 int gprx_ctx_create(int device, gprx_ctx** out);
@@ -120,8 +126,9 @@ int gprx_batch_run(gprx_batch* batch, const double* theta, unsigned flags, doubl
  * var == NULL: mean only.                                                                      */
 int gprx_batch_predict(gprx_batch* batch, double* mu, double* var);
 int gprx_batch_dims(const gprx_batch* batch, int* B, int* d, int* N, int* M_max);
-/* alpha = K^-1 (y - mean) of the last successful factorisation, alpha[b*N + t] (GPE's gp.alpha;
- * N doubles per slot), for hosts that keep GaussianProcesses' own fields current.              */
+/* alpha = K^-1 (y - mean) of the last factorisation, alpha[b*N + t] (GPE's gp.alpha; N doubles
+ * per slot), for hosts that keep GaussianProcesses' own fields current.  A slot whose status in
+ * that evaluation was not GPRX_OK has no alpha: its N entries are NaN.                          */
 int gprx_batch_alpha(gprx_batch* batch, double* alpha);
 
 /* ---- hyper-parameter optimisation on the device ------------------------------------------- */
@@ -145,7 +152,8 @@ typedef struct gprx_opt_options {
   int iterations;     /* Options.iterations (1000)                                               */
   int max_evals;      /* Options.f_calls_limit, the deterministic budget: a soft limit on f calls
                          (the initial evaluation + every line-search trial = the device evaluations),
-                         checked after each iteration; < 0: none (default)                        */
+                         checked after each iteration; <= 0: none (default;
+                         Optim's f_calls_limit = 0)                        */
   int ls_iterations;  /* BackTracking.iterations (1000)                                          */
   int scaleinvH0;     /* LBFGS scaleinvH0 (true)                                                 */
   int refit;          /* 1: end with one evaluation of every slot at its minimiser, as optimize!
@@ -171,6 +179,9 @@ void gprx_opt_defaults(gprx_opt_options* opt);
  * time_limit is one wall clock for the whole call (all slots), not per GP as Optim's per-call
  * Options(time_limit=10.) at CPnoise.jl:41.  The context's mutex is held for the whole call:
  * other threads sharing the context wait until the optimisation ends.                         */
+/* Outputs are written when the call returns GPRX_OK or a refit status after the search.  A call
+ * rejected before the search (no training data, options out of range: GPRX_INVALID_ARGUMENT)
+ * and a device / memory error write none of them.                                               */
 int gprx_batch_optimize(gprx_batch* batch, const double* theta0, const gprx_opt_options* opt, double* theta_out,
                         double* minimum, int* iterations, int* f_calls, int* g_calls, int* stopped, int* rounds);
 

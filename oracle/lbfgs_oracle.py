@@ -25,9 +25,9 @@ Conventions restated:
   * The objective is get_optim_target's -mll; a failed evaluation is +Inf with a NaN gradient.
   * dot products: sequential sums of products in index order (the order the product kernels use;
     Julia's BLAS ddot block order is not part of any pinned source).
-  * LineSearches' `iterfinite` counter starts at 0 here (at most iterfinitemax = 52 halvings for
-    non-finite trial values); the product restatements start it at 1 (51 halvings).  Only a run
-    of 51 consecutive non-finite trials could tell them apart; the tests never reach it.
+  * LineSearches' `iterfinite` counter starts at 0 (at most iterfinitemax = 52 halvings for
+    non-finite trial values), as in LineSearches 7.1.1; both product restatements
+    (gprx/optim.py, gprx_lbfgs.hip) start it at 0 too since round 2.
 """
 from __future__ import annotations
 

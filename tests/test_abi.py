@@ -35,6 +35,31 @@ def test_abi_version_and_status_strings():
     assert L.lib.gprx_status_string(1) == b"not positive definite"
 
 
+def test_library_is_built_from_the_shipped_sources(tmp_path):
+    """gprx_build_id() = the hash gpr.jl_amd/Makefile takes of the sources; the loader refuses a
+    library whose id differs from the sources next to it (a stale prebuilt libgprx.so)."""
+    assert L.lib.gprx_build_id().decode() == L.source_build_id()
+    assert len(L.source_build_id()) == 16
+    # a changed source gives another id
+    import hashlib
+
+    root = L._HERE.parent
+    h = hashlib.sha256()
+    for i, f in enumerate(L.BUILD_SOURCES):
+        b = (root / f).read_bytes()
+        h.update(b + (b" " if i == 0 else b""))
+    assert h.hexdigest()[:16] != L.source_build_id()
+
+
+def test_device_count_without_gpu():
+    import torch
+
+    if torch.cuda.device_count() > 0:
+        assert L.lib.gprx_device_count() == torch.cuda.device_count()
+    else:
+        assert L.lib.gprx_device_count() == 0
+
+
 def test_cstate_pack_bit_exact():
     rng = np.random.default_rng(0)
     nb = 4
@@ -99,3 +124,21 @@ def test_optimizer_defaults_and_null_handle():
     assert math.isnan(o.time_limit) and math.isnan(op.time_limit)
     th = (C.c_double * 4)()
     assert L.lib.gprx_batch_optimize(None, th, C.byref(o), None, None, None, None, None, None, None) == L.INVALID_ARGUMENT
+
+
+def test_optimizer_options_are_validated_on_the_host():
+    """gprx.batch.opt_options rejects what gprx_batch_optimize would (ValueError before any call)
+    and maps Options(max_evals=None) to Optim's f_calls_limit = 0 (no limit)."""
+    import math
+
+    from gprx.batch import opt_options
+    from gprx.optim import LBFGS, BackTracking, Options
+
+    o = opt_options()
+    assert o.m == 10 and o.max_evals == 0 and o.refit == 1 and math.isnan(o.time_limit)
+    assert opt_options(options=Options(max_evals=30), refit=False).max_evals == 30
+    for kw in (dict(method=LBFGS(m=65)), dict(method=LBFGS(m=0)), dict(options=Options(iterations=-1)),
+               dict(options=Options(successive_f_tol=-1)), dict(method=LBFGS(alphaguess=math.nan)),
+               dict(method=LBFGS(linesearch=BackTracking(order=3))), dict(options=Options(g_abstol=math.nan))):
+        with pytest.raises(ValueError):
+            opt_options(**kw)

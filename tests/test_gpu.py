@@ -709,6 +709,55 @@ def test_device_optimize_refit_failure_is_reported(gprx, ctx, golden_dir):
     b.close()
 
 
+def test_device_optimize_rejects_invalid_options(gprx, ctx, golden_dir):
+    """Invalid options are rejected before the search: ValueError from the Python side; through the
+    raw C ABI GPRX_INVALID_ARGUMENT with every output left unwritten (distinguishable from a refit
+    failure, which fills the outputs); the batch is still usable afterwards."""
+    import ctypes as C
+
+    from gprx import _lib as L
+    from gprx.optim import LBFGS, Options
+
+    z = np.load(golden_dir / "p1_n50.npz")
+    X, Y, th = z["X"], z["Y"], z["theta"]
+    b = gprx.GPBatch(2, X.shape[0], X.shape[1], 0, ctx=ctx)
+    b.set_train(X, Y[:2])
+    th0 = np.stack([th, th])
+    for bad in (dict(method=LBFGS(m=65)), dict(method=LBFGS(m=0)), dict(options=Options(iterations=-1)),
+                dict(method=LBFGS(alphaguess=math.inf))):
+        with pytest.raises(ValueError):
+            b.optimize(th0, **bad)
+    o = gprx.batch.opt_options()
+    o.m = 100
+    stp = np.full(2, -7, dtype=np.int32)
+    th_out = np.full((2, th.shape[0]), 123.0)
+    rc = L.lib.gprx_batch_optimize(b.h, L.dptr(th0), C.byref(o), L.dptr(th_out), None, None, None, None, L.iptr(stp),
+                                   None)
+    assert rc == L.INVALID_ARGUMENT
+    assert np.all(stp == -7) and np.all(th_out == 123.0)
+    res, _ = b.optimize(th0, LBFGS(), Options(max_evals=5))
+    assert all(r.f_calls >= 1 for r in res)
+    b.close()
+
+
+def test_alpha_of_a_failed_slot_is_nan(gprx, ctx, golden_dir):
+    """gprx_batch_alpha: alpha is defined only for the slots whose last evaluation succeeded; a
+    failed slot (not positive definite) reads NaN, the others the oracle's alpha."""
+    z = np.load(golden_dir / "nonpd_p1.npz")
+    X, Y, th = z["X"], z["Y"], z["theta"]
+    good = th.copy()
+    good[0] = -2.0
+    b = gprx.GPBatch(2, X.shape[0], X.shape[1], 0, ctx=ctx)
+    b.set_train(X, Y[:2])
+    r = b.run(np.stack([th, good]))
+    assert r["status"][0] == 1 and r["status"][1] == 0
+    a = b.alpha()
+    assert np.all(np.isnan(a[0]))
+    f = O.fit(X, Y[1], good, None, ctx.dist_mode)
+    np.testing.assert_allclose(a[1], f["alpha"], rtol=0, atol=1e-9 * np.max(np.abs(f["alpha"])))
+    b.close()
+
+
 def test_alpha_export_matches_oracle(gprx, ctx, golden_dir):
     """gprx_batch_alpha (gp.alpha for hosts that keep GaussianProcesses' fields current) equals
     the oracle's alpha = K^-1 y; before any factorisation it answers NOT_READY."""

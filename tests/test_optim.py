@@ -68,6 +68,16 @@ def test_max_evals_budget_is_deterministic():
     np.testing.assert_array_equal(r1.minimizer, r2.minimizer)
 
 
+def test_max_evals_zero_is_no_limit():
+    """Optim: f_limit_reached = f_calls_limit > 0 && ... -- a budget of 0 (Optim's default) or
+    less is no limit, not a stop after the first iteration."""
+    free = lbfgs_minimize(rosen, rosen_fg, np.array([-1.2, 1.0]))
+    for lim in (0, -1):
+        r = lbfgs_minimize(rosen, rosen_fg, np.array([-1.2, 1.0]), options=Options(max_evals=lim))
+        assert r.stopped_by == free.stopped_by == "g_tol" and r.f_calls == free.f_calls
+        np.testing.assert_array_equal(r.minimizer, free.minimizer)
+
+
 def test_lbfgs_improves_gp_target(golden_dir):
     z = np.load(golden_dir / "p1_n50.npz")
     X, y, th0 = z["X"], z["Y"][0], z["theta"]

@@ -146,9 +146,11 @@ def test_sweep_run_gathers_through_a_process_group(ctx):
         dist.destroy_process_group()
     assert set(res["results"]["noisy"]) == {"P2_MIN16", "P2_MAX16", "CP_MIN16", "CP_MAX16"}
     e = res["results"]["noisy"]["P2_MIN16"]
-    assert e["nprocessed"] == 4 and len(e["kstep_mse"]) == 4
     r = sweep.run_group("P2", 16, "min", range(4), ctx, TESTS, STEPS, 10)
-    np.testing.assert_array_equal([math.inf if v is None else v for v in e["kstep_mse"]], r["kstep_mse"])
+    # failed trials are dropped from the lists (core.jl:41-53), nprocessed still counts them
+    assert e["nprocessed"] == 4 and len(e["kstep_mse"]) == 4 - int(r["failed"].sum()) == 4 - e["dropped"]
+    np.testing.assert_array_equal(e["kstep_mse"], r["kstep_mse"][~r["failed"]])
+    assert len(e["projectionerror"]) == len(e["kstep_mse"])
 
 
 def test_fb_hyperparameter_optimise_n4096(ctx):
