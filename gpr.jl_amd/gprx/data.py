@@ -163,16 +163,18 @@ def _noisy(mech: str, m: dict, rng) -> dict:
     return m
 
 
-def make_trial(mech: str, N: int, M: int = 100, seed: int = 0) -> dict:
+def make_trial(mech: str, N: int, M: int = 100, seed: int = 0, noise: bool = True) -> dict:
     """One trial's training/test data.  Returns X (d,N), Xcurr (d,N), Y (G,N), Xs (d,M),
-    idx (1-based output coordinates), d."""
+    idx (1-based output coordinates), d.  noise=False: the simulated states as the datasets hold
+    them (hyperparameter.jl applies no noise; noise.jl does, applynoise! at e.g. CPnoise.jl:23)."""
     rng = np.random.default_rng(seed)
+    nz = (lambda m, r: _noisy(mech, m, r)) if noise else (lambda m, r: m)
     m_old = _sample_minimal(mech, N, rng)
     m_cur = _step(mech, m_old)
-    X = _cstates(mech, _noisy(mech, m_old, rng))
-    Xcurr = _cstates(mech, _noisy(mech, m_cur, rng))
+    X = _cstates(mech, nz(m_old, rng))
+    Xcurr = _cstates(mech, nz(m_cur, rng))
     rng_t = np.random.default_rng(seed + 500000)
-    Xs = _cstates(mech, _noisy(mech, _sample_minimal(mech, M, rng_t), rng_t)) if M > 0 else None
+    Xs = _cstates(mech, nz(_sample_minimal(mech, M, rng_t), rng_t)) if M > 0 else None
     idx = VW_INDICES[mech]
     Y = np.stack([Xcurr[i - 1, :] for i in idx], axis=0)
     return dict(X=X, Xcurr=Xcurr, Y=Y, Xs=Xs, idx=idx, d=X.shape[0])
@@ -203,19 +205,20 @@ def min_features(mech: str, q: np.ndarray, usesin: bool) -> np.ndarray:
     return np.stack(rows, axis=0)
 
 
-def make_trial_min(mech: str, N: int, M: int = 100, seed: int = 0, usesin: bool = False) -> dict:
+def make_trial_min(mech: str, N: int, M: int = 100, seed: int = 0, usesin: bool = False, noise: bool = True) -> dict:
     """One minimal-coordinate trial: X (d, N) inputs at the noisy old states, Y (nc, N) the noisy
     next-step rates (ytrain = [[s[id] for s in xtrain_curr] for id in [2,4]], P2noise.jl(min):30),
-    start (M, 2nc) the noisy test states (xtest_old, :33)."""
+    start (M, 2nc) the noisy test states (xtest_old, :33).  noise=False as for make_trial."""
     rng = np.random.default_rng(seed)
+    nz = (lambda m, r: _noisy(mech, m, r)) if noise else (lambda m, r: m)
     m_old = _sample_minimal(mech, N, rng)
     m_cur = _step(mech, m_old)
-    old, cur = _noisy(mech, m_old, rng), _noisy(mech, m_cur, rng)
+    old, cur = nz(m_old, rng), nz(m_cur, rng)
     keys = MIN_COORDS[mech]
     q_old = np.stack([old[k] for pair in keys for k in pair], axis=1)
     Y = np.stack([cur[rate] for _, rate in keys], axis=0)
     rng_t = np.random.default_rng(seed + 500000)
-    tst = _noisy(mech, _sample_minimal(mech, M, rng_t), rng_t)
+    tst = nz(_sample_minimal(mech, M, rng_t), rng_t)
     start = np.stack([tst[k] for pair in keys for k in pair], axis=1)
     X = min_features(mech, q_old, usesin)
     return dict(X=X, Y=Y, start=start, d=X.shape[0])

@@ -31,6 +31,28 @@ from typing import Callable, Sequence
 import numpy as np
 
 
+def init_ranks(rehearse: bool = False) -> int:
+    """One process per GPU under torch.distributed.run: bind this rank to GPU LOCAL_RANK and, for a
+    world size > 1, join the RCCL (`nccl`) group.  More ranks than visible GPUs is an error unless
+    `rehearse` (ranks then share devices over a gloo group: a rehearsal, never a measurement).
+    Returns the world size."""
+    import os
+
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = torch.cuda.device_count()
+    if ndev < 1 or (world > ndev and not rehearse):
+        raise SystemExit(f"gprx: {world} rank(s) need {world} GPUs, {ndev} visible (rehearse=True shares devices)")
+    torch.cuda.set_device(local % ndev)
+    if world > 1:
+        backend = "gloo" if rehearse else "nccl"
+        _dist().init_process_group(backend)
+        assert _dist().get_backend() == backend and _dist().get_world_size() == world
+    return world
+
+
 def shard_trials(n_trials: int, rank: int, world: int) -> list[int]:
     """Trial-major round robin (the mapping core.jl's threads get, by jobid mod ngpu)."""
     return list(range(rank, n_trials, world))

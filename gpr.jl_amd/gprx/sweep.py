@@ -72,12 +72,15 @@ def local_trials(mech: str, N: int, variant: str, trial_ids, testsamples: int) -
 
 
 def run_group(mech: str, N: int, variant: str, trial_ids, ctx, testsamples: int = 100, simsteps: int = 20,
-              max_evals: int | None = 30, time_limit: float = float("nan"), keep: bool = False) -> dict:
+              max_evals: int | None = 30, time_limit: float = float("nan"), keep: bool = False,
+              trials: list | None = None) -> dict:
     """One (mechanism, N, variant) group for this rank's trials: device optimise of every GP,
-    then the variant's evaluation.  Returns per-trial arrays (n_local, ...) and timings."""
+    then the variant's evaluation.  Returns per-trial arrays (n_local, ...) and timings.
+    trials: prebuilt local_trials-shaped inputs (the hyper-parameter search's), else noise.jl's."""
     from .optim import LBFGS, Options
 
-    trials = local_trials(mech, N, variant, trial_ids, testsamples)
+    if trials is None:
+        trials = local_trials(mech, N, variant, trial_ids, testsamples)
     n = len(trials)
     if n == 0:
         return {}
@@ -203,16 +206,9 @@ def main(argv=None):
     ap.add_argument("--max-evals", type=int, default=30, help="evaluation budget per GP (<0: none)")
     ap.add_argument("--time-limit", type=float, default=float("nan"), help="seconds per group call (NaN: none)")
     ap.add_argument("--out", default="gpurun_out/sweep_final_checkpoint.json")
+    ap.add_argument("--rehearse", action="store_true", help="allow ranks to share GPUs (gloo control plane)")
     a = ap.parse_args(argv)
-    import torch
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
-    if world > 1:
-        import torch.distributed as dist
-
-        dist.init_process_group("nccl" if torch.cuda.device_count() >= world else "gloo")
+    world = shard.init_ranks(a.rehearse)
     t0 = time.perf_counter()
     res = run([m for m in a.mechs.split(",") if m], [int(s) for s in a.sizes.split(",") if s],
               [v for v in a.variants.split(",") if v], a.trials, a.testsamples, a.simsteps,

@@ -154,27 +154,24 @@ def test_sweep_run_gathers_through_a_process_group(ctx):
 
 
 def test_fb_hyperparameter_optimise_n4096(ctx):
-    """examples/hyperparameter.jl:50-60 -> FBparam.jl shape at the BASELINE size: FB, N=4096,
-    d=52, the 12 output GPs of one trial, random-restart start theta (CPparam.jl:28-31: theta =
-    [100, 50 ./ std(X)] jittered), MeanZero, device LBFGS + BackTracking(order=2) with a
-    30-evaluation budget.  The LML at the minimisers against the oracle; the optimiser improves
-    every slot it does not fail on."""
+    """examples/hyperparameter.jl:50-60 -> experimentFBMax (maximal_coordinates/FBparam.jl:23-33)
+    at the BASELINE size: FB, N=4096, d=52, the 12 output GPs of one trial, all starting from the
+    trial's ONE random draw params = [1, 10 ./ std(X)] .+ (5rand .- 0.999) .* params (gprx.search),
+    MeanZero, device LBFGS + BackTracking(order=2) with a 30-evaluation budget.  The LML at the
+    minimisers against the oracle; the optimiser improves every slot it does not fail on."""
     import gprx
-    from gprx import data
+    from gprx import data, search
     from gprx.optim import LBFGS, Options
 
-    tr = data.make_trial("FB", 4096, 0, seed=data.trial_seed("FB", 1))
+    tr = data.make_trial("FB", 4096, 0, seed=data.trial_seed("FB", 1), noise=False)
     X, Y = tr["X"], tr["Y"]
     G = Y.shape[0]
-    rng = np.random.default_rng(4096)
+    p = search.init_params("FB_MAX", X, search.draw_rng("FB_MAX", 4096, 1))
     stdx = X.std(axis=1, ddof=1)
     stdx[stdx == 0] = 1000.0
-    p0 = np.concatenate([[100.0], 50.0 / stdx])
-    th0 = []
-    for _ in range(G):
-        p = p0 + (5 * rng.random(p0.shape[0]) - 0.999) * p0
-        th0.append(data.theta_from_params(p))
-    th0 = np.stack(th0)
+    base = np.concatenate([[1.0], 10.0 / stdx])
+    assert np.all((p >= 0.001 * base - 1e-12) & (p <= 5.001 * base + 1e-12))  # (5 rand - 0.999) jitter
+    th0 = np.tile(data.theta_from_params(p), (G, 1))  # one draw shared by all 12 outputs
     b = gprx.GPBatch(G, 52, 4096, 0, ctx=ctx)
     b.set_train(X, Y)
     start = b.run(th0, grad=False)
