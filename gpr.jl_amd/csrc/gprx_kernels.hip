@@ -303,7 +303,7 @@ struct Frag4 {
 };
 // NB < QN: only the first NB 16-column blocks of B (the prediction's last, partly padded test tile)
 template <int NB = QN>
-__device__ __forceinline__ void frag4_load(Frag4& f, const double* pa, const double* pb, size_t sa, size_t sb) {
+__device__ __forceinline__ void frag4_load(Frag4& f, const double* pa, const double* pb, ptrdiff_t sa, ptrdiff_t sb) {
 #pragma unroll
   for (int s = 0; s < Q4SD; ++s) {
 #pragma unroll
@@ -321,20 +321,25 @@ __device__ __forceinline__ void frag4_mma(d4 (&acc)[QM][QN], const Frag4& f) {
 #pragma unroll
       for (int b = 0; b < NB; ++b) acc[a][b] = mfma(f.b[s][b], f.a[s][a], acc[a][b]);
 }
-template <int NB = QN>
+// REV: the K range is walked from its end down (any k order is a valid summation order; the MFMA
+// k-slices only have to pair the same k in A and B).  Ops whose units share the END of their K
+// range but not its start (TT, the lauum) then stream the same k-slab at the same time on the
+// co-resident workgroups of a slot, so the slab is served from the XCD's L2.
+template <int NB = QN, bool REV = false>
 __device__ __forceinline__ void mma_64x64(d4 (&acc)[QM][QN], const double* __restrict__ A, size_t lda,
                                           const double* __restrict__ B, size_t ldb, int K) {
   const int nst = __builtin_amdgcn_readfirstlane(K / (4 * Q4SD));  // even: K is whole 64-tiles
   if (nst <= 0) return;
   const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
-  const double* pa = A + lr + (size_t)lk * lda;
-  const double* pb = B + lr + (size_t)lk * ldb;
-  const size_t sa = 4 * lda, sb = 4 * ldb;
+  const int k0 = REV ? K - 4 + lk : lk;  // first k-slice of this lane
+  const double* pa = A + lr + (ptrdiff_t)k0 * (ptrdiff_t)lda;
+  const double* pb = B + lr + (ptrdiff_t)k0 * (ptrdiff_t)ldb;
+  const ptrdiff_t sa = (REV ? -4 : 4) * (ptrdiff_t)lda, sb = (REV ? -4 : 4) * (ptrdiff_t)ldb;
   Frag4 f0, f1;
   frag4_load<NB>(f0, pa, pb, sa, sb);
   for (int it = 0; it < nst; it += 2) {
     __builtin_amdgcn_sched_barrier(0);
-    frag4_load<NB>(f1, pa + (size_t)(it + 1) * Q4SD * sa, pb + (size_t)(it + 1) * Q4SD * sb, sa, sb);
+    frag4_load<NB>(f1, pa + (ptrdiff_t)(it + 1) * Q4SD * sa, pb + (ptrdiff_t)(it + 1) * Q4SD * sb, sa, sb);
     frag4_mma<NB>(acc, f0);
 #pragma unroll
     for (int g = 0; g < Q4SD * (QM + NB); ++g) {
@@ -343,7 +348,7 @@ __device__ __forceinline__ void mma_64x64(d4 (&acc)[QM][QN], const double* __res
     }
     __builtin_amdgcn_sched_barrier(0);
     const int n2 = (it + 2 < nst) ? it + 2 : nst - 1;
-    frag4_load<NB>(f0, pa + (size_t)n2 * Q4SD * sa, pb + (size_t)n2 * Q4SD * sb, sa, sb);
+    frag4_load<NB>(f0, pa + (ptrdiff_t)n2 * Q4SD * sa, pb + (ptrdiff_t)n2 * Q4SD * sb, sa, sb);
     frag4_mma<NB>(acc, f1);
 #pragma unroll
     for (int g = 0; g < Q4SD * (QM + NB); ++g) {
@@ -427,6 +432,32 @@ __device__ __forceinline__ void mma_64x16_ldsb(d4 (&acc)[QM], const double* __re
       for (int q = 0; q < QM; ++q) acc[q] = mfma(b[s], a[s][q], acc[q]);
   }
 }
+// ---- diagnostic build only (-DGPRX_STAMPS, scratch/clock.py): the in-kernel clock of a main loop
+// (MI355X_MICROARCH.md 'DVFS give-back' item 6): s_memtime (shader cycles) and s_memrealtime
+// (100 MHz) before and after, per wave, into a buffer no other code reads.  Not in the product build.
+#ifdef GPRX_STAMPS
+constexpr int STAMP_MAX = 1 << 18;  // waves per stamp region
+__device__ unsigned long long g_stamps[2][STAMP_MAX][4];
+struct Stamp {
+  unsigned long long t, r;
+};
+__device__ __forceinline__ Stamp stamp_now() {
+  __builtin_amdgcn_sched_barrier(0);
+  Stamp s{__builtin_amdgcn_s_memtime(), __builtin_amdgcn_s_memrealtime()};
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only
+  __builtin_amdgcn_sched_barrier(0);
+  return s;
+}
+__device__ __forceinline__ void stamp_store(int region, const Stamp& a, const Stamp& b) {
+  const size_t i = (size_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if ((threadIdx.x & 63) == 0 && i < STAMP_MAX) {
+    g_stamps[region][i][0] = a.t;
+    g_stamps[region][i][1] = b.t;
+    g_stamps[region][i][2] = a.r;
+    g_stamps[region][i][3] = b.r;
+  }
+}
+#endif
 __device__ __forceinline__ void acc4_zero(d4 (&acc)[QM][QN]) {
 #pragma unroll
   for (int a = 0; a < QM; ++a)
@@ -879,7 +910,19 @@ __device__ __forceinline__ void gemm_tile(const DevBatch& db, const GemmGeom& g,
     else if (nbv == 2) mma_64x64<2>(acc, Ak, ld, Bk, ldb, (ke - kb) * TS);
     else mma_64x64<1>(acc, Ak, ld, Bk, ldb, (ke - kb) * TS);
   } else {
-    mma_64x64(acc, Ak, ld, Bk, ldb, (ke - kb) * TS);
+#ifdef GPRX_STAMPS
+    const Stamp st0 = stamp_now();
+#endif
+    if (op == OP_TT)  // K = [ti, o + h): the units of a launch share the end
+      mma_64x64<QN, true>(acc, Ak, ld, Bk, ldb, (ke - kb) * TS);
+    else
+      mma_64x64(acc, Ak, ld, Bk, ldb, (ke - kb) * TS);
+#ifdef GPRX_STAMPS
+    if ((op == OP_SYRK || op == OP_TT) && g.n == db.nt) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      stamp_store(1, st0, stamp_now());
+    }
+#endif
   }
   if (PV) {  // OP_PREDVAR runs only in the k_gemm_pv instance
 #pragma unroll
@@ -1468,9 +1511,18 @@ __device__ __forceinline__ void lauum_unit(const DevBatch& db, int slot, const i
   d4 acc[QM][QN];
   acc4_zero(acc);
   const size_t ld = db.ld, so = (size_t)slot * db.mat;
+#ifdef GPRX_STAMPS
+  const Stamp st0 = stamp_now();
+#endif
   if (active)
-    mma_64x64(acc, db.Mt + so + (size_t)ti * TS * ld + ti * TS, ld, db.Mt + so + (size_t)ti * TS * ld + tj * TS, ld,
-              (nt - ti) * TS);
+    mma_64x64<QN, true>(acc, db.Mt + so + (size_t)ti * TS * ld + ti * TS, ld, db.Mt + so + (size_t)ti * TS * ld + tj * TS,
+                        ld, (nt - ti) * TS);  // K = [ti, nt): reversed, every unit starts at the shared end
+#ifdef GPRX_STAMPS
+  if (active && (ju - db.lauum_order) % (2 * LU) == 0) {  // the job's first (long) unit
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stamp_store(0, st0, stamp_now());
+  }
+#endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA landed
   __syncthreads();                                   // ... and every other wave's
   double sf = 0.0, tr = 0.0;
@@ -2050,3 +2102,17 @@ void launch_rollout(const RolloutArgs& a, int dist_mode, hipStream_t s) {
 }
 
 }  // namespace gprx
+
+#ifdef GPRX_STAMPS
+// diagnostic build only: copy (reset = 0) or clear (reset = 1) stamp region `which`
+extern "C" int gprx_dbg_stamps(int which, unsigned long long* out, long long n, int reset) {
+  void* p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(gprx::g_stamps)) != hipSuccess) return 3;
+  char* base = (char*)p + (size_t)which * sizeof(gprx::g_stamps[0]);
+  const size_t bytes = std::min<size_t>((size_t)n * 8, sizeof(gprx::g_stamps[0]));
+  if (hipDeviceSynchronize() != hipSuccess) return 3;
+  if (reset) return hipMemset(base, 0, sizeof(gprx::g_stamps[0])) == hipSuccess ? 0 : 3;
+  return hipMemcpy(out, base, bytes, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 3;
+}
+#endif
+

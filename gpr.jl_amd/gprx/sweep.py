@@ -16,14 +16,20 @@ rolls out every test trajectory of every local trial in one launch (gprx_rollout
 are gathered as raw tensors (shard.gather_results) and written in the shape of the reference's
 final checkpoint (core.jl:79-82): {etype: {ID<N>: {nprocessed, kstep_mse[], projectionerror[]}}}.
 
-Variants (the MeanZero half of noise.jl's six; the MeanDynamics half runs CPU physics per
-training column, SURVEY.md section 2 rows 3/22, out of scope):
+Variants (all of noise.jl:72-85):
     max      maximal coordinates, CState inputs (experiment_*_mz_max): optimise + 20-step device
              predictdynamics (GP means, projectv!, updatestate!: gprx.projection), error =
              simulationerror of the final CStates, projectionerror = the mean projection error
     min      minimal coordinates (experiment_*_mz_min): optimise + 20-step device rollout, error =
              simulationerror of the final CStates (position MSE)
     min_sin  as min with (sin, cos) angle features (experiment_*_mz_min_sin)
+    vi       the physics-only baseline (noise.jl:72-75, examples/baseline.jl): the noisy test starts
+             simulated by the variational integrator alone (gprx.vi.simulate), no GP
+    md_*     the same three with MeanDynamics GPs (experiment_*_md_*): the prior mean is one
+             variational-integrator step (gprx.vi / gprx.mdynamics), computed once per training
+             set for the fit (y - mu(X) on the device) and at every rollout step's states; the
+             GP means of a rollout step come from one batched device predict, the projection
+             from the device
 Data are the synthetic generator's (gprx.data; the .jls datasets are absent), seeded per
 (mechanism, trial) as 1000 * config_id + trial (data.trial_seed).
 """
@@ -38,12 +44,15 @@ import time
 import numpy as np
 
 from . import data, shard
+from . import mdynamics
 from .rollout import NCOORD, final_cstate, rollout_min
 
 MECHS = ("P1", "P2", "CP", "FB")
 SIZES = (2, 4, 8, 16, 32, 64, 128, 256, 512)  # noise.jl:64
-VARIANTS = ("max", "min", "min_sin")
-ETYPE = {"max": "noisy", "min": "noisy", "min_sin": "noisysin"}  # parallelsim idmod (noise.jl:82-84)
+VARIANTS = ("vi", "max", "min", "min_sin", "md_max", "md_min", "md_min_sin")  # noise.jl:72-85 order
+# parallelsim idmod (noise.jl:80-85): etype = "noisy" * idmod
+ETYPE = {"max": "noisy", "min": "noisy", "min_sin": "noisysin", "md_max": "noisyMD", "md_min": "noisyMD",
+         "md_min_sin": "noisyMDsin"}
 
 
 def _dist():
@@ -55,19 +64,29 @@ def _dist():
 def local_trials(mech: str, N: int, variant: str, trial_ids, testsamples: int) -> list[dict]:
     """The trials' GP inputs, built on the rank that owns them."""
     out = []
+    md = variant.startswith("md_")
+    base = variant[3:] if md else variant
     for t in trial_ids:
         seed = data.trial_seed(mech, t)
-        if variant == "max":
+        if base == "max":
             tr = data.make_trial(mech, N, testsamples, seed=seed)
             th = data.theta0(mech, N, "MAX")
-            out.append(dict(X=tr["X"], Y=tr["Y"], Xs=tr["Xs"], theta=np.tile(th, (tr["Y"].shape[0], 1)), trial=t,
-                            seed=seed))
+            d = dict(X=tr["X"], Y=tr["Y"], Xs=tr["Xs"], theta=np.tile(th, (tr["Y"].shape[0], 1)), trial=t, seed=seed)
+            if md:  # MeanDynamics prior mean, once per training set (gprx.mdynamics)
+                d["mu"] = mdynamics.mean_max(mech, tr["X"])
         else:
-            usesin = variant == "min_sin"
+            usesin = base == "min_sin"
             tr = data.make_trial_min(mech, N, testsamples, seed=seed, usesin=usesin)
             th = data.theta0_min(mech, N, usesin)
-            out.append(dict(X=tr["X"], Y=tr["Y"], Xs=None, start=tr["start"], theta=np.tile(th, (tr["Y"].shape[0], 1)),
-                            trial=t, seed=seed))
+            d = dict(X=tr["X"], Y=tr["Y"], Xs=None, start=tr["start"], theta=np.tile(th, (tr["Y"].shape[0], 1)),
+                     trial=t, seed=seed)
+            if md:  # the rollout predicts at the test starts' features with the batch's test capacity
+                d["mu"] = mdynamics.mean_min(mech, tr["X"], usesin)
+                d["Xs"] = data.min_features(mech, tr["start"], usesin)
+        if md:
+            d["Y_raw"] = d["Y"]
+            d["Y"] = d["Y"] - d["mu"]  # the device fits y - μ(X) (mDynamics.jl: θ-independent mean)
+        out.append(d)
     return out
 
 
@@ -114,8 +133,30 @@ def run_group(mech: str, N: int, variant: str, trial_ids, ctx, testsamples: int 
                     continue
                 truth = data.test_truth(mech, testsamples, trials[i]["seed"], simsteps)["X"].T
                 err[i] = data.position_mse(truth, fin[sl])
-                perr[i] = float(np.mean(pe[sl]))
-                failed[i] = False  # projectionerror / length(xtest_old) (P2noise.jl:51)
+                perr[i] = float(np.mean(pe[sl]))  # projectionerror / length(xtest_old) (P2noise.jl:51)
+                failed[i] = False
+    elif variant == "md_max":
+        # predictdynamics with MeanDynamics GPs: GP means on the device + the physics mean per step
+        good = [i for i in range(n) if np.all(ok_gp[i])]
+        if good:
+            starts = np.stack([trials[i]["Xs"].T for i in range(n)])  # (n, M, d)
+            fin, pe, st = mdynamics.rollout_max(mech, rb, good, starts, simsteps, ctx=ctx)
+            for k, i in enumerate(good):
+                if np.any(st[k] != 0):
+                    continue
+                truth = data.test_truth(mech, testsamples, trials[i]["seed"], simsteps)["X"].T
+                err[i] = data.position_mse(truth, fin[k])
+                perr[i] = float(np.mean(pe[k]))
+                failed[i] = False
+    elif variant in ("md_min", "md_min_sin"):
+        good = [i for i in range(n) if np.all(ok_gp[i])]
+        if good:
+            starts = np.stack([trials[i]["start"] for i in range(n)])  # (n, M, 2 nc)
+            fin = mdynamics.rollout_min(mech, rb, good, starts, simsteps, usesin=variant == "md_min_sin")
+            for k, i in enumerate(good):
+                truth = data.test_truth(mech, testsamples, trials[i]["seed"], simsteps)["X"].T
+                err[i] = data.position_mse(truth, fin[k])
+                failed[i] = False
     else:
         usesin = variant == "min_sin"
         nc = NCOORD[mech]
@@ -142,6 +183,21 @@ def run_group(mech: str, N: int, variant: str, trial_ids, ctx, testsamples: int 
     return out
 
 
+def run_vi_baseline(mech: str, trial_ids, testsamples: int = 100, simsteps: int = 20) -> dict:
+    """The pure variational-integrator baseline (noise.jl:72-75, examples/baseline.jl:3-16
+    experimentVarInt): every noisy test start simulated for simsteps + 1 physics steps
+    (gprx.vi.simulate), error = simulationerror against the noise-free truth.  Host physics, no GP."""
+    from . import vi
+
+    err = np.full(len(trial_ids), math.inf)
+    for k, t in enumerate(trial_ids):
+        seed = data.trial_seed(mech, t)
+        start = data.make_trial(mech, 2, testsamples, seed=seed)["Xs"].T
+        fin, _ = vi.simulate(mech, start, simsteps)
+        err[k] = data.position_mse(data.test_truth(mech, testsamples, seed, simsteps)["X"].T, fin)
+    return dict(kstep_mse=err)
+
+
 def run(mechs=MECHS, sizes=SIZES, variants=VARIANTS, n_trials: int = 100, testsamples: int = 100, simsteps: int = 20,
         max_evals: int | None = 30, time_limit: float = float("nan"), ctx=None, log=None) -> dict:
     """The sweep.  Every rank runs its trials of every group; rank 0 returns the gathered
@@ -158,8 +214,24 @@ def run(mechs=MECHS, sizes=SIZES, variants=VARIANTS, n_trials: int = 100, testsa
     results: dict = {}
     timing: dict = {}
     for mech in mechs:
+        if "vi" in variants:  # the pure variational-integrator baseline (noise.jl:72-75, idmod "VI")
+            t0 = time.perf_counter()
+            r = run_vi_baseline(mech, mine, testsamples, simsteps)
+            loc = {"kstep_mse": r["kstep_mse"].reshape(-1, 1), "t": np.full((len(mine), 1), time.perf_counter() - t0)}
+            g = shard.gather_results(loc, n_trials, lambda q: shard.shard_trials(n_trials, q, world), 0,
+                                     keys=("kstep_mse", "t")) if dist else loc
+            if rank == 0:
+                results.setdefault("noisyVI", {})[f"{mech}_MIN2"] = {
+                    "nprocessed": n_trials, "kstep_mse": [float(v) for v in g["kstep_mse"][:, 0]],
+                    "projectionerror": [0.0] * n_trials, "variant": "vi"}
+                timing[f"{mech}_MIN2/vi"] = {"seconds_max_rank": float(np.max(g["t"][:, 0])) if n_trials else 0.0,
+                                             "gp_fits": 0}
+                if log:
+                    log(f"{mech}_MIN2 vi: {timing[f'{mech}_MIN2/vi']['seconds_max_rank']:.3f} s")
         for N in sizes:
             for var in variants:
+                if var == "vi":
+                    continue
                 r = run_group(mech, N, var, mine, ctx, testsamples, simsteps, max_evals, time_limit)
                 local = {"kstep_mse": r.get("kstep_mse", np.zeros(0)), "perr": r.get("projectionerror", np.zeros(0)),
                          "failed": r.get("failed", np.zeros(0, dtype=bool)).astype(np.float64),
@@ -171,7 +243,7 @@ def run(mechs=MECHS, sizes=SIZES, variants=VARIANTS, n_trials: int = 100, testsa
                                              keys=("kstep_mse", "perr", "failed", "ok", "t"))
                 else:
                     g = {k: v.reshape(-1, 1) for k, v in local.items()}
-                key = f"{mech}_{'MAX' if var == 'max' else 'MIN'}{N}"
+                key = f"{mech}_{'MAX' if var.endswith('max') else 'MIN'}{N}"
                 if rank == 0:
                     # failed trials are left out of both lists (core.jl:41-53), nprocessed counts them;
                     # a non-finite error of a trial that ran (a diverged rollout) is kept as the
@@ -184,7 +256,7 @@ def run(mechs=MECHS, sizes=SIZES, variants=VARIANTS, n_trials: int = 100, testsa
                                                        "variant": var, "ok": int(g["ok"][:, 0].sum()),
                                                        "dropped": int((~keep).sum())}
                     timing[f"{key}/{var}"] = {"seconds_max_rank": float(np.max(g["t"][:, 0])) if n_trials else 0.0,
-                                              "gp_fits": n_trials * (len(data.VW_INDICES[mech]) if var == "max"
+                                              "gp_fits": n_trials * (len(data.VW_INDICES[mech]) if var.endswith("max")
                                                                      else NCOORD[mech])}
                     if log:
                         log(f"{key} {var}: ok {results[et][key]['ok']}/{n_trials}, "

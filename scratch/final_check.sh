@@ -17,3 +17,5 @@ rc=0; timeout -k 10 120 python bench.py --gpus 2 --no-cpu --no-opt > gpurun_out/
 echo "bench --gpus 2 on one GPU: rc=$rc (expected 2)"
 timeout -k 10 600 python bench.py --gpus 2 --rehearse --steps 3 --warmup 1 --no-cpu --no-opt > gpurun_out/final_bench2.json 2> gpurun_out/final_bench2.err
 echo "2-rank rehearsal ok"
+if [ -n "$LEVELS" ]; then timeout -k 10 300 python scratch/levels.py 40 3 > gpurun_out/final_levels.txt 2>&1; echo "levels ok"; fi
+if [ -n "$CLOCK" ]; then GPRX_LIB=scratch/var/libgprx_stamps.so timeout -k 10 300 python scratch/clock.py 40 3 > gpurun_out/final_clock.txt 2>&1; echo "clock ok"; fi

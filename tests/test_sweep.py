@@ -50,7 +50,7 @@ def test_reduced_sweep_against_oracle(ctx, mech):
 
     mode = ctx.dist_mode
     for N in SIZES:
-        for var in sweep.VARIANTS:
+        for var in ("max", "min", "min_sin"):  # the MeanDynamics ones: test_meandynamics_variants_against_oracle
             r = sweep.run_group(mech, N, var, range(TRIALS), ctx, testsamples=TESTS, simsteps=STEPS, max_evals=20,
                                 keep=True)
             rb, trials = r["rb"], r["trials"]
@@ -189,3 +189,79 @@ def test_fb_hyperparameter_optimise_n4096(ctx):
         ok, info = _mll_ok(r["mll"][s], X, Y[s], thmin[s], ctx.dist_mode)
         assert ok, (s, info)
     b.close()
+
+
+@pytest.mark.parametrize("mech", ("P2", "CP"))
+def test_meandynamics_variants_against_oracle(ctx, mech):
+    """noise.jl's experiment_*_md_max / _md_min / _md_min_sin (MeanDynamics GPs) through the product
+    path (gprx.sweep.run_group -> gprx.mdynamics): mu(X) once per training set against the
+    independent action-based VI oracle, the LML at the device minimisers against the oracle GP on
+    y - mu(X), and the rollouts (GP mean + physics mean per step; projectv! for maximal
+    coordinates) against an oracle loop (oracle GP means, oracle VI, oracle projection)."""
+    from gprx import data, mdynamics, sweep
+    from gprx.rollout import final_cstate
+    from oracle import projection_oracle as PO
+    from oracle import vi_oracle as VO
+
+    mode = ctx.dist_mode
+    N, M, steps = 16, 4, 3
+    for var in ("md_max", "md_min", "md_min_sin"):
+        r = sweep.run_group(mech, N, var, range(2), ctx, testsamples=M, simsteps=steps, max_evals=10, keep=True)
+        rb, trials = r["rb"], r["trials"]
+        tr = trials[0]
+        usesin = var == "md_min_sin"
+        # the physics mean of the first training column against the oracle
+        if var == "md_max":
+            o, _ = VO.vi_step(mech, tr["X"][:, 0])
+            mu_o = o[np.asarray(data.VW_INDICES[mech]) - 1]
+        else:
+            o, _ = VO.vi_step(mech, mdynamics.xtransform(mech, tr["X"][:, :1], usesin)[0])
+            mu_o = (np.array([o[10], o[23] - o[10]]) if mech == "P2"
+                    else o[np.asarray(mdynamics.MIN_IDX[mech]) - 1])
+        np.testing.assert_allclose(tr["mu"][:, 0], mu_o, rtol=0, atol=1e-9)
+        assert np.all(r["status"][0] == 0)
+        G = rb.G
+        th = r["theta"][0]
+        for g in range(G):
+            ok, info = _mll_ok(r["mll"][0, g], tr["X"], tr["Y"][g], th[g], mode)
+            assert ok, (var, g, info)
+        al = [O.fit(tr["X"], tr["Y"][g], th[g], None, mode)["alpha"] for g in range(G)]
+
+        def gp_mean(feat):
+            out = []
+            for g in range(G):
+                il2, sf2 = np.exp(-2 * th[g][1:-1]), np.exp(2 * th[g][-1])
+                D = O.dist_stack(tr["X"], feat[:, None], mode)
+                out.append(float((sf2 * np.exp(-0.5 * np.einsum("pij,p->ij", D, il2)))[:, 0] @ al[g]))
+            return np.array(out)
+
+        if var == "md_max":
+            starts = np.stack([t["Xs"].T for t in trials])
+            fin, pe, st = mdynamics.rollout_max(mech, rb, [0], starts, steps, ctx=ctx)
+            assert np.all(st == 0)
+            for j in range(2):
+                def predict(obs):
+                    s, _ = VO.vi_step(mech, obs)
+                    return gp_mean(obs) + s[np.asarray(data.VW_INDICES[mech]) - 1]
+
+                ref, perr = PO.predictdynamics(mech, predict, starts[0, j], steps, data.VW_INDICES[mech])
+                np.testing.assert_allclose(fin[0, j], ref, rtol=0, atol=1e-7)
+                assert abs(pe[0, j] - perr) <= 1e-7 * max(1.0, perr)
+        else:
+            starts = np.stack([t["start"] for t in trials])
+            fin = mdynamics.rollout_min(mech, rb, [0], starts, steps, usesin)
+            for j in range(2):
+                q_old, qd_old = starts[0, j, 0::2].copy(), starts[0, j, 1::2].copy()
+                q_cur = q_old + 0.01 * qd_old
+                for _ in range(steps):
+                    obs = np.empty(2 * len(q_old))
+                    obs[0::2], obs[1::2] = q_old, qd_old
+                    feat = data.min_features(mech, obs[None, :], usesin)[:, 0]
+                    o, _ = VO.vi_step(mech, mdynamics.xtransform(mech, feat[:, None], usesin)[0])
+                    mo = (np.array([o[10], o[23] - o[10]]) if mech == "P2"
+                          else o[np.asarray(mdynamics.MIN_IDX[mech]) - 1])
+                    rates = gp_mean(feat) + mo
+                    q_old, qd_old = q_cur, rates
+                    q_cur = q_cur + 0.01 * rates
+                np.testing.assert_allclose(fin[0, j], final_cstate(mech, q_cur), rtol=0, atol=1e-9)
+        rb.close()
