@@ -321,22 +321,15 @@ __device__ __forceinline__ void frag4_mma(d4 (&acc)[QM][QN], const Frag4& f) {
 #pragma unroll
       for (int b = 0; b < NB; ++b) acc[a][b] = mfma(f.b[s][b], f.a[s][a], acc[a][b]);
 }
-// REV: the K range is walked from its end down (any k order is a valid summation order; the MFMA
-// k-slices only have to pair the same k in A and B).  Ops whose units share the END of their K
-// range but not its start (TT, the lauum) then stream the same k-slab at the same time on the
-// co-resident workgroups of a slot, so the slab is served from the XCD's L2.
-// rev is a run-time (wave-uniform) flag, so the kernels hold one copy of the core.
 template <int NB = QN>
 __device__ __forceinline__ void mma_64x64(d4 (&acc)[QM][QN], const double* __restrict__ A, size_t lda,
-                                          const double* __restrict__ B, size_t ldb, int K, bool rev = false) {
+                                          const double* __restrict__ B, size_t ldb, int K) {
   const int nst = __builtin_amdgcn_readfirstlane(K / (4 * Q4SD));  // even: K is whole 64-tiles
   if (nst <= 0) return;
   const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
-  const int dir = __builtin_amdgcn_readfirstlane(rev ? -4 : 4);
-  const int k0 = (rev ? K - 4 : 0) + lk;  // first k-slice of this lane
-  const double* pa = A + lr + (ptrdiff_t)k0 * (ptrdiff_t)lda;
-  const double* pb = B + lr + (ptrdiff_t)k0 * (ptrdiff_t)ldb;
-  const ptrdiff_t sa = (ptrdiff_t)dir * (ptrdiff_t)lda, sb = (ptrdiff_t)dir * (ptrdiff_t)ldb;
+  const double* pa = A + lr + (ptrdiff_t)lk * (ptrdiff_t)lda;
+  const double* pb = B + lr + (ptrdiff_t)lk * (ptrdiff_t)ldb;
+  const ptrdiff_t sa = 4 * (ptrdiff_t)lda, sb = 4 * (ptrdiff_t)ldb;
   Frag4 f0, f1;
   frag4_load<NB>(f0, pa, pb, sa, sb);
   for (int it = 0; it < nst; it += 2) {
@@ -915,8 +908,7 @@ __device__ __forceinline__ void gemm_tile(const DevBatch& db, const GemmGeom& g,
 #ifdef GPRX_STAMPS
     const Stamp st0 = stamp_now();
 #endif
-    // TT: K = [ti, o + h), the units of a launch share the end: walked from it
-    mma_64x64(acc, Ak, ld, Bk, ldb, (ke - kb) * TS, op == OP_TT);
+    mma_64x64(acc, Ak, ld, Bk, ldb, (ke - kb) * TS);
 #ifdef GPRX_STAMPS
     if ((op == OP_SYRK || op == OP_TT) && g.n == db.nt) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1516,7 +1508,7 @@ __device__ __forceinline__ void lauum_unit(const DevBatch& db, int slot, const i
 #endif
   if (active)
     mma_64x64(acc, db.Mt + so + (size_t)ti * TS * ld + ti * TS, ld, db.Mt + so + (size_t)ti * TS * ld + tj * TS, ld,
-              (nt - ti) * TS, true);  // K = [ti, nt): reversed, every unit starts at the shared end
+              (nt - ti) * TS);
 #ifdef GPRX_STAMPS
   if (active && (ju - db.lauum_order) % (2 * LU) == 0) {  // the job's first (long) unit
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

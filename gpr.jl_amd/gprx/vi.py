@@ -253,45 +253,47 @@ def vi_step(mech_name: str, cstates, dt: float = DT, eps: float = 1e-10, newton_
     it = np.zeros(T, dtype=np.int32)
     done = np.zeros(T, dtype=bool)
 
-    def residual(v2, w2, lam):
-        Jw2 = np.einsum("bij,tbj->tbi", J, w2)
-        sq2 = np.sqrt(4.0 / dt ** 2 - np.sum(w2 * w2, axis=-1))
-        dT = m[None, :, None] * ((v2 - v1) / dt + np.array([0.0, 0.0, GRAV]))
-        dR = sq2[..., None] * Jw2 + np.cross(w2, Jw2) - mom1
-        d = np.concatenate([dT, dR], axis=-1).reshape(T, n6) - np.einsum("tcj,tc->tj", Gpos, lam)
-        x3 = x2 + v2 * dt
-        q3 = step_q(q2, w2, dt)
+    def residual(a, v2a, w2a, lama):
+        """residual of the states a (index array) at (v2a, w2a, lama)"""
+        Jw2 = np.einsum("bij,tbj->tbi", J, w2a)
+        sq2 = np.sqrt(4.0 / dt ** 2 - np.sum(w2a * w2a, axis=-1))
+        dT = m[None, :, None] * ((v2a - v1[a]) / dt + np.array([0.0, 0.0, GRAV]))
+        dR = sq2[..., None] * Jw2 + np.cross(w2a, Jw2) - mom1[a]
+        d = np.concatenate([dT, dR], axis=-1).reshape(len(a), n6) - np.einsum("tcj,tc->tj", Gpos[a], lama)
+        x3 = x2[a] + v2a * dt
+        q3 = step_q(q2[a], w2a, dt)
         return np.concatenate([d, constraints(mech, x3, q3)], axis=1), Jw2, sq2, x3, q3
 
+    a = np.arange(T)  # the states still iterating (converged ones drop out)
     for k in range(1, newton_iter + 1):
-        f, Jw2, sq2, x3, q3 = residual(v2, w2, lam)
-        F = np.zeros((T, n6 + nd, n6 + nd))
+        na = len(a)
+        f, Jw2, sq2, x3, q3 = residual(a, v2[a], w2[a], lam[a])
+        F = np.zeros((na, n6 + nd, n6 + nd))
         for b in range(nb):
             o = 6 * b
             F[:, o:o + 3, o:o + 3] = np.eye(3) * (m[b] / dt)
             # d/dw2 [(sq2 I + [w2 x]) J w2]
-            F[:, o + 3:o + 6, o + 3:o + 6] = (sq2[:, b, None, None] * J[b] + skew(w2[:, b]) @ J[b]
-                                              - skew(Jw2[:, b])
-                                              - Jw2[:, b, :, None] * w2[:, b, None, :] / sq2[:, b, None, None])
-        F[:, :n6, n6:] = -np.swapaxes(Gpos, 1, 2)
+            wb = w2[a, b]
+            F[:, o + 3:o + 6, o + 3:o + 6] = (sq2[:, b, None, None] * J[b] + skew(wb) @ J[b] - skew(Jw2[:, b])
+                                              - Jw2[:, b, :, None] * wb[:, None, :] / sq2[:, b, None, None])
+        F[:, :n6, n6:] = -np.swapaxes(Gpos[a], 1, 2)
         Gphi3 = jac_phi(mech, x3, q3)
-        Gvel = np.zeros((T, nd, n6))
         for b in range(nb):
             o = 6 * b
-            Gvel[:, :, o:o + 3] = Gphi3[:, :, o:o + 3] * dt
-            Gvel[:, :, o + 3:o + 6] = Gphi3[:, :, o + 3:o + 6] @ _dphi_dw(q2[:, b], q3[:, b], w2[:, b], dt)
-        F[:, n6:, :n6] = Gvel
+            F[:, n6:, o:o + 3] = Gphi3[:, :, o:o + 3] * dt
+            F[:, n6:, o + 3:o + 6] = Gphi3[:, :, o + 3:o + 6] @ _dphi_dw(q2[a, b], q3[:, b], w2[a, b], dt)
         if reg:
             F[:, n6:, n6:] -= reg * np.eye(nd)
         ds = np.linalg.solve(F, f[..., None])[..., 0]
-        ds[done] = 0.0
-        v2 = v2 - ds[:, :n6].reshape(T, nb, 6)[..., 0:3]
-        w2 = w2 - ds[:, :n6].reshape(T, nb, 6)[..., 3:6]
-        lam = lam - ds[:, n6:]
-        it[~done] = k
-        fn = np.linalg.norm(residual(v2, w2, lam)[0], axis=1)
-        done |= (fn < eps) & (np.linalg.norm(ds, axis=1) < eps)
-        if done.all():
+        v2[a] -= ds[:, :n6].reshape(na, nb, 6)[..., 0:3]
+        w2[a] -= ds[:, :n6].reshape(na, nb, 6)[..., 3:6]
+        lam[a] -= ds[:, n6:]
+        it[a] = k
+        fn = np.linalg.norm(residual(a, v2[a], w2[a], lam[a])[0], axis=1)
+        conv = (fn < eps) & (np.linalg.norm(ds, axis=1) < eps)
+        done[a[conv]] = True
+        a = a[~conv]
+        if len(a) == 0:
             break
     out = np.concatenate([x2, q2, v2, w2], axis=-1).reshape(T, 13 * nb)
     return out, it, (~done).astype(np.int32)

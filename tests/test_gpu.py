@@ -433,18 +433,19 @@ def test_mean_only_prediction_matches_full(gprx, ctx, golden_dir):
 
 
 def test_fb_full_size_n4096_d52(gprx, ctx):
-    """BASELINE config FB: N=4096, d=52, the 12 per-output GPs of one trial with a theta-independent
-    prior mean subtracted (MeanDynamics role), M=100 test states.  Two slots against the oracle
-    (mll to the flat 1e-10 relative bound, gradient, mean, variance), every slot finite and
-    bit-identical across repeated runs.  The prior mean 0.05 x[8] is synthetic: the experiments'
-    MeanDynamics physics is out of scope, and any theta-independent mean enters the
-    device path the same way, as y - mu(X)."""
-    from gprx import data
+    """BASELINE config FB "with mDynamics variational-integrator mean": N=4096, d=52, the 12
+    per-output GPs of one trial with the MeanDynamics prior mean subtracted (mu(X): one
+    variational-integrator step per training state, gprx.mdynamics.mean_max -- getμ(vωindices) of
+    experiment_fb_md_max, FBnoise.jl), M=100 test states.  Two slots against the oracle (mll to the
+    flat 1e-10 relative bound, gradient, mean, variance), every slot finite and bit-identical across
+    repeated runs."""
+    from gprx import data, mdynamics
 
     tr = data.make_trial("FB", 4096, 100, seed=data.trial_seed("FB", 0))
     th = data.theta0("FB", 512)  # the largest FB key of config.json
     G = tr["Y"].shape[0]
-    mu0 = 0.05 * tr["X"][8]  # a theta-independent prior mean over the training states
+    mu0 = mdynamics.mean_max("FB", tr["X"])  # (12, 4096), theta-independent
+    assert np.all(np.isfinite(mu0))
     Y = tr["Y"] - mu0
     b = gprx.GPBatch(G, 52, 4096, 100, ctx=ctx)
     b.set_train(tr["X"], Y)

@@ -163,7 +163,9 @@ def test_fb_hyperparameter_optimise_n4096(ctx):
     from gprx import data, search
     from gprx.optim import LBFGS, Options
 
-    tr = data.make_trial("FB", 4096, 0, seed=data.trial_seed("FB", 1), noise=False)
+    # the generator's noisy states: its noise-free four-bar targets are an exact function of the
+    # inputs, which drives sigma_n -> 0 and cond(K) past what an LML comparison can resolve
+    tr = data.make_trial("FB", 4096, 0, seed=data.trial_seed("FB", 1))
     X, Y = tr["X"], tr["Y"]
     G = Y.shape[0]
     p = search.init_params("FB_MAX", X, search.draw_rng("FB_MAX", 4096, 1))
