@@ -353,6 +353,191 @@ __device__ __forceinline__ void mma_64x64(d4 (&acc)[QM][QN], const double* __res
     __builtin_amdgcn_sched_barrier(0);
   }
 }
+// mma_64x64 with triangular operand tiles and lower-only outputs skipped at 16 x 16-block
+// granularity.  A 64-K tile of the K loop is 8 stages (k = 8s..8s+7), i.e. 4 loop trips of 2 stages.
+//   TRI_A_FIRST  A's first K tile is upper triangular (explicit zeros below the diagonal): row block
+//                a is zero for k < 16a, so trip t of that tile needs rows a <= t (lauum: A = Mt[ti, ti:];
+//                TT: A = Mt[ti, ti:]).
+//   TRI_AB_FIRST the same with B = A (a diagonal output tile of the lauum), and only the output blocks
+//                b <= a are formed (the caller ignores the upper ones): trip t needs blocks a, b <= t.
+//   LOWER_SAME   B = A (a diagonal SYRK tile): only the blocks b <= a, dense operands.
+//   TRI_A_LAST   A's last K tile is lower triangular: row block a is zero for k > 16a + 15, so trip t
+//                of that tile needs rows a >= t (LINV21: A = Linv[ti, :ti]).
+//   TRI_B_LAST   the same for B's column blocks (TRSM: B = Linv[tj, :tj]).
+// The peeled trips carry compile-time masks; skipped products are exact zeros, so the sums are
+// bit-identical to the full core's.  Shared panels (B = A) load the fragments once.
+enum CoreMode { PLAIN = 0, TRI_A_FIRST, TRI_AB_FIRST, LOWER_SAME, TRI_A_LAST, TRI_B_LAST, REV_A, REV_B };
+template <int A0, int A1, int B0, int B1, bool SAME>
+__device__ __forceinline__ void frag4_load_r(Frag4& f, const double* pa, const double* pb, ptrdiff_t sa, ptrdiff_t sb) {
+  constexpr int L0 = SAME ? (A0 < B0 ? A0 : B0) : A0, L1 = SAME ? (A1 > B1 ? A1 : B1) : A1;
+#pragma unroll
+  for (int s = 0; s < Q4SD; ++s) {
+#pragma unroll
+    for (int a = L0; a < L1; ++a) f.a[s][a] = pa[s * sa + 16 * a];
+    if constexpr (!SAME) {
+#pragma unroll
+      for (int b = B0; b < B1; ++b) f.b[s][b] = pb[s * sb + 16 * b];
+    }
+  }
+}
+template <int A0, int A1, int B0, int B1, bool SAME, bool LOWER>
+__device__ __forceinline__ void frag4_mma_r(d4 (&acc)[QM][QN], const Frag4& f) {
+#pragma unroll
+  for (int s = 0; s < Q4SD; ++s)
+#pragma unroll
+    for (int a = A0; a < A1; ++a)
+#pragma unroll
+      for (int b = B0; b < B1; ++b) {
+        if (LOWER && b > a) continue;
+        acc[a][b] = mfma(SAME ? f.a[s][b] : f.b[s][b], f.a[s][a], acc[a][b]);
+      }
+}
+// masks of trip T (0..3) of the triangular tile; T = 4: the dense trips
+template <int MODE, int T>
+struct TripMask {
+  static constexpr bool first = MODE == TRI_A_FIRST || MODE == TRI_AB_FIRST || MODE == REV_A || MODE == REV_B;
+  static constexpr bool dense = T >= 4 || (first && T == 3);
+  static constexpr int a0 = (!dense && MODE == TRI_A_LAST) ? T : (!dense && MODE == REV_A) ? 3 - T : 0;
+  static constexpr int a1 = (!dense && (MODE == TRI_A_FIRST || MODE == TRI_AB_FIRST)) ? T + 1 : QM;
+  static constexpr int b0 = (!dense && MODE == TRI_B_LAST) ? T : (!dense && MODE == REV_B) ? 3 - T : 0;
+  static constexpr int b1 = (!dense && MODE == TRI_AB_FIRST) ? T + 1 : QN;
+};
+template <int MODE, int T>
+__device__ __forceinline__ void core_load(Frag4& f, const double* pa, const double* pb, ptrdiff_t sa, ptrdiff_t sb,
+                                          int st) {
+  constexpr bool same = MODE == TRI_AB_FIRST || MODE == LOWER_SAME;
+  using M = TripMask<MODE, T>;
+  frag4_load_r<M::a0, M::a1, M::b0, M::b1, same>(f, pa + (ptrdiff_t)st * Q4SD * sa, pb + (ptrdiff_t)st * Q4SD * sb, sa, sb);
+}
+template <int MODE, int T>
+__device__ __forceinline__ void core_mma(d4 (&acc)[QM][QN], const Frag4& f) {
+  using M = TripMask<MODE, T>;
+  constexpr bool same = MODE == TRI_AB_FIRST || MODE == LOWER_SAME;
+  frag4_mma_r<M::a0, M::a1, M::b0, M::b1, same, same>(acc, f);
+}
+// group barriers of a dense half trip: one load per two MFMAs (shared panels: 8 loads, 20 MFMAs)
+template <int MODE>
+__device__ __forceinline__ void core_groups() {
+  if constexpr (MODE == TRI_AB_FIRST || MODE == LOWER_SAME) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+    }
+  } else {
+#pragma unroll
+    for (int g = 0; g < Q4SD * (QM + QN); ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+    }
+  }
+}
+template <int MODE>
+__device__ __forceinline__ void mma_64x64_m(d4 (&acc)[QM][QN], const double* __restrict__ A, size_t lda,
+                                            const double* __restrict__ B, size_t ldb, int K) {
+  const int nst = __builtin_amdgcn_readfirstlane(K / (4 * Q4SD));  // multiple of 8: K is whole 64-tiles
+  if (nst <= 0) return;
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  const double* pa = A + lr + (ptrdiff_t)lk * (ptrdiff_t)lda;
+  const double* pb = B + lr + (ptrdiff_t)lk * (ptrdiff_t)ldb;
+  const ptrdiff_t sa = 4 * (ptrdiff_t)lda, sb = 4 * (ptrdiff_t)ldb;
+  constexpr bool first = MODE == TRI_A_FIRST || MODE == TRI_AB_FIRST;
+  constexpr bool last = MODE == TRI_A_LAST || MODE == TRI_B_LAST;
+  Frag4 f0, f1;
+  // one peeled trip T of the triangular tile, stages st and st + 1; the prefetch of stage st + 2
+  // uses trip T2's masks (NX: whether there is a next stage at all)
+#define GPRX_TRIP(M, T, T2, st, NX)                       \
+  {                                                       \
+    __builtin_amdgcn_sched_barrier(0);                    \
+    core_load<M, T>(f1, pa, pb, sa, sb, (st) + 1);        \
+    core_mma<M, T>(acc, f0);                              \
+    __builtin_amdgcn_sched_barrier(0);                    \
+    if (NX) core_load<M, T2>(f0, pa, pb, sa, sb, (st) + 2); \
+    core_mma<M, T>(acc, f1);                              \
+  }
+  int it = 0, end = nst;
+  if constexpr (first) {
+    core_load<MODE, 0>(f0, pa, pb, sa, sb, 0);
+    GPRX_TRIP(MODE, 0, 1, 0, true)
+    GPRX_TRIP(MODE, 1, 2, 2, true)
+    GPRX_TRIP(MODE, 2, 3, 4, true)
+    it = 6;
+  } else {
+    core_load<MODE, last ? 0 : 4>(f0, pa, pb, sa, sb, 0);
+    if constexpr (last) end = nst - 8;
+  }
+  for (; it < end; it += 2) {
+    __builtin_amdgcn_sched_barrier(0);
+    core_load<MODE, 4>(f1, pa, pb, sa, sb, it + 1);
+    core_mma<MODE, 4>(acc, f0);
+    core_groups<MODE>();
+    __builtin_amdgcn_sched_barrier(0);
+    const int n2 = (it + 2 < nst) ? it + 2 : nst - 1;
+    core_load<MODE, 4>(f0, pa, pb, sa, sb, n2);
+    core_mma<MODE, 4>(acc, f1);
+    core_groups<MODE>();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if constexpr (last) {  // the triangular last tile; f0 holds its stage 0 (dense masks)
+    const int st = end;
+    GPRX_TRIP(MODE, 0, 1, st, true)
+    GPRX_TRIP(MODE, 1, 2, st + 2, true)
+    GPRX_TRIP(MODE, 2, 3, st + 4, true)
+    GPRX_TRIP(MODE, 3, 3, st + 6, false)
+  }
+  __builtin_amdgcn_sched_barrier(0);
+}
+// k_gemm's core: ONE copy of the dense loop and at most one peeled prefix per kernel instance (a
+// second inlined copy of the loop, or a second peeled prefix / tail, makes the register allocator
+// spill 150-700 VGPRs).  The instance's op (PM) has its triangular tile peeled in front of the
+// loop: TT walks K forward from its upper-triangular first tile (Mt[ti,ti]); TRSM and LINV21 walk
+// K backward from their lower-triangular last tile (Linv[tj,tj], Linv[ti,ti]: reversed trip T
+// needs the row / column blocks >= 3 - T).  tri: this wave's op is PM's.
+template <int PM>
+__device__ __forceinline__ void mma_64x64_pm(d4 (&acc)[QM][QN], const double* __restrict__ A, size_t lda,
+                                             const double* __restrict__ B, size_t ldb, int K, bool tri) {
+  const int nst = __builtin_amdgcn_readfirstlane(K / (4 * Q4SD));
+  if (nst <= 0) return;
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  const double* pa = A + lr + (ptrdiff_t)lk * (ptrdiff_t)lda;
+  const double* pb = B + lr + (ptrdiff_t)lk * (ptrdiff_t)ldb;
+  ptrdiff_t sa = 4 * (ptrdiff_t)lda, sb = 4 * (ptrdiff_t)ldb;
+  Frag4 f0, f1;
+  int it = 0;
+  if (tri) {
+    if constexpr (PM == REV_A || PM == REV_B) {  // sub-step j reads k-block K/4 - 1 - j
+      pa += (ptrdiff_t)(nst * Q4SD - 1) * sa;
+      pb += (ptrdiff_t)(nst * Q4SD - 1) * sb;
+      sa = -sa;
+      sb = -sb;
+    }
+    core_load<PM, 0>(f0, pa, pb, sa, sb, 0);
+    GPRX_TRIP(PM, 0, 1, 0, true)
+    GPRX_TRIP(PM, 1, 2, 2, true)
+    GPRX_TRIP(PM, 2, 3, 4, true)
+    it = 6;
+  } else {
+    core_load<PLAIN, 4>(f0, pa, pb, sa, sb, 0);
+  }
+  for (; it < nst; it += 2) {
+    __builtin_amdgcn_sched_barrier(0);
+    core_load<PLAIN, 4>(f1, pa, pb, sa, sb, it + 1);
+    core_mma<PLAIN, 4>(acc, f0);
+    core_groups<PLAIN>();
+    __builtin_amdgcn_sched_barrier(0);
+    const int n2 = (it + 2 < nst) ? it + 2 : nst - 1;
+    core_load<PLAIN, 4>(f0, pa, pb, sa, sb, n2);
+    core_mma<PLAIN, 4>(acc, f1);
+    core_groups<PLAIN>();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+#undef GPRX_TRIP
 // 64 x 16 wave core (the fused leaf's column-quarter tasks): acc[a] += A(64 x K) B(16 x K)^T,
 // lane l reg q = C[16a + (l&15)][(l>>4) + 4q]; 4 MFMAs per 5 fragment loads, stages of depth 16
 // in ping-pong (the same barriers as mma_64x64, groups of 5 loads and 4 MFMAs interleaved: leaf
@@ -863,7 +1048,7 @@ __device__ __forceinline__ void diag_tile_fast(const DevBatch& db, int slot, int
 // ============================================================================================
 // One 64 x 64 output tile (ti, tj) of a GemmOp on one wave.
 constexpr int TT_S = TS + 2;  // row stride of k_gemm's per-wave transpose buffer (LINV21's Mt store)
-template <bool PV>
+template <bool PV, int PM = PLAIN>
 __device__ __forceinline__ void gemm_tile(const DevBatch& db, const GemmGeom& g, int slot, int ti, int tj) {
   const int op = PV ? (int)OP_PREDVAR : g.op;
   const size_t ld = db.ld, so = (size_t)slot * db.mat;
@@ -908,7 +1093,11 @@ __device__ __forceinline__ void gemm_tile(const DevBatch& db, const GemmGeom& g,
 #ifdef GPRX_STAMPS
     const Stamp st0 = stamp_now();
 #endif
-    mma_64x64(acc, Ak, ld, Bk, ldb, (ke - kb) * TS);
+    // the operands' triangular tiles (diagonal tiles of Linv / Mt) and SYRK's upper blocks of a
+    // diagonal tile are skipped (mma_64x64_m); op and ti == tj are wave-uniform
+    const int Kn = (ke - kb) * TS;
+    const bool tri = (PM == TRI_A_FIRST && op == OP_TT) || (PM == REV_A && op == OP_LINV21) || (PM == REV_B && op == OP_TRSM);
+    mma_64x64_pm<PM>(acc, Ak, ld, Bk, ldb, Kn, tri);
 #ifdef GPRX_STAMPS
     if ((op == OP_SYRK || op == OP_TT) && g.n == db.nt) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -972,7 +1161,7 @@ __device__ __forceinline__ void gemm_tile(const DevBatch& db, const GemmGeom& g,
   }
 }
 
-template <bool PV>
+template <bool PV, int PM = PLAIN>
 __device__ __forceinline__ void gemm_body(const DevBatch& db, const GemmGeom& g1, const GemmGeom& g2) {
   int r0, c0, R, C, r02, c02, R2, C2;
   bool tri, tri2;
@@ -991,13 +1180,13 @@ __device__ __forceinline__ void gemm_body(const DevBatch& db, const GemmGeom& g1
   unit_shape(op, UR, UC);
   int np = 1, pr2 = 0, pc2 = 0;  // second (folded) unit
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (tri) {  // lower-triangle tile 4u + w in row-major order
+  int wr = w / UC, wc = w - wr * UC;
+  if (tri) {  // lower-triangle tile 4u + w in row-major order (one call site of gemm_tile below:
+              // its cores are inlined once)
     const int t = 4 * u + w;
     if (t >= R * (R + 1) / 2) return;  // wave-uniform: the last unit's missing tiles
-    int i, j;
-    quad_tri(t, i, j);
-    gemm_tile<PV>(db, g, slot, __builtin_amdgcn_readfirstlane(r0 + i), __builtin_amdgcn_readfirstlane(c0 + j));
-    return;
+    quad_tri(t, pr, pc);
+    wr = wc = 0;
   } else {
     const int RU = (R + UR - 1) / UR, CU = (C + UC - 1) / UC;
     if (op == OP_SYRK) {
@@ -1018,13 +1207,12 @@ __device__ __forceinline__ void gemm_body(const DevBatch& db, const GemmGeom& g1
       np = (lo != hi) ? 2 : 1;
     }
   }
-  const int wr = w / UC, wc = w - wr * UC;
 #pragma unroll 1
   for (int pass = 0; pass < np; ++pass) {
     const int ur = pass ? pr2 : pr, uc = pass ? pc2 : pc;
     if (ur + wr >= R || uc + wc >= C) continue;  // wave-uniform: partial unit
     // wave-uniform tile indices in SGPRs (the 64 x 64 core needs every VGPR)
-    gemm_tile<PV>(db, g, slot, __builtin_amdgcn_readfirstlane(r0 + ur + wr), __builtin_amdgcn_readfirstlane(c0 + uc + wc));
+    gemm_tile<PV, PM>(db, g, slot, __builtin_amdgcn_readfirstlane(r0 + ur + wr), __builtin_amdgcn_readfirstlane(c0 + uc + wc));
   }
 }
 
@@ -1182,8 +1370,11 @@ __device__ __forceinline__ void gemm_tile_pair(const DevBatch& db, const GemmGeo
 __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_gemm_p(DevBatch db, GemmGeom g, GemmGeom g2) {
   gemm_body_pair(db, g, g2);
 }
+// PM: the op whose triangular operand tile the instance peels (TRI_A_FIRST: TT of the SYRK + TT
+// launches; REV_B: TRSM; REV_A: LINV21)
+template <int PM>
 __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_gemm(DevBatch db, GemmGeom g, GemmGeom g2) {
-  gemm_body<false>(db, g, g2);
+  gemm_body<false, PM>(db, g, g2);
 }
 __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_gemm_pv(DevBatch db, GemmGeom g, GemmGeom g2) {
   gemm_body<true>(db, g, g2);
@@ -1506,9 +1697,11 @@ __device__ __forceinline__ void lauum_unit(const DevBatch& db, int slot, const i
 #ifdef GPRX_STAMPS
   const Stamp st0 = stamp_now();
 #endif
-  if (active)
-    mma_64x64(acc, db.Mt + so + (size_t)ti * TS * ld + ti * TS, ld, db.Mt + so + (size_t)ti * TS * ld + tj * TS, ld,
-              (nt - ti) * TS);
+  if (active) {  // wave-uniform: diagonal tiles form only their lower blocks
+    const double* Ap = db.Mt + so + (size_t)ti * TS * ld + ti * TS;
+    if (ti == tj) mma_64x64_m<TRI_AB_FIRST>(acc, Ap, ld, Ap, ld, (nt - ti) * TS);
+    else mma_64x64_m<TRI_A_FIRST>(acc, Ap, ld, db.Mt + so + (size_t)ti * TS * ld + tj * TS, ld, (nt - ti) * TS);
+  }
 #ifdef GPRX_STAMPS
   if (active && (ju - db.lauum_order) % (2 * LU) == 0) {  // the job's first (long) unit
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2061,7 +2254,9 @@ void launch_gemm(const DevBatch& b, const GemmGeom& g, hipStream_t s, const Gemm
   if (g2.op != OP_NONE) T += op_units(g2, b.nt, b.mt);
   const size_t lds = (g.op == OP_LINV21 || g2.op == OP_LINV21) ? 4 * 16 * TT_S * sizeof(double) : 0;
   if (g.op == OP_PREDVAR) hipLaunchKernelGGL(k_gemm_pv, dim3(grid_blocks(b.B, T)), dim3(NTHR), lds, s, b, g, g2);
-  else hipLaunchKernelGGL(k_gemm, dim3(grid_blocks(b.B, T)), dim3(NTHR), lds, s, b, g, g2);
+  else if (g.op == OP_TRSM) hipLaunchKernelGGL(k_gemm<REV_B>, dim3(grid_blocks(b.B, T)), dim3(NTHR), lds, s, b, g, g2);
+  else if (g.op == OP_LINV21) hipLaunchKernelGGL(k_gemm<REV_A>, dim3(grid_blocks(b.B, T)), dim3(NTHR), lds, s, b, g, g2);
+  else hipLaunchKernelGGL(k_gemm<TRI_A_FIRST>, dim3(grid_blocks(b.B, T)), dim3(NTHR), lds, s, b, g, g2);
 }
 void launch_alpha(const DevBatch& b, hipStream_t s, int phase) {
   hipLaunchKernelGGL(k_alpha, dim3(grid_blocks(b.B, b.nt)), dim3(NTHR), 0, s, b, phase);

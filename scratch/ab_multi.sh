@@ -2,11 +2,11 @@
 # A/B/C...: the in-tree library and each GPRX_LIB given as an argument, alternating, twice;
 # prints ms_per_step and the per-kernel ms of the bench (no CPU / optimiser legs)
 set -e
-for i in 1 2; do
+for i in $(seq 1 ${REPS:-2}); do
   for v in in-tree "$@"; do
     if [ $v = in-tree ]; then unset GPRX_LIB; else export GPRX_LIB=$v; fi
     tag=$(basename $v .so)$i
-    timeout -k 10 200 python bench.py --steps 5 --no-cpu --no-opt > gpurun_out/abm_$tag.log 2>&1
+    timeout -k 10 200 python bench.py --steps ${STEPS:-5} --no-cpu --no-opt > gpurun_out/abm_$tag.log 2>&1
     python -c "
 import json
 for l in open('gpurun_out/abm_$tag.log'):
