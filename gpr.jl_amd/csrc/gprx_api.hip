@@ -481,6 +481,7 @@ int gprx_batch_create(gprx_ctx* c, int B, int d, int N, int M_max, gprx_batch** 
   if ((rc = dalloc(b, &db.Xc, Bs * db.Npad * db.xs))) return fail(rc);
   if ((rc = dalloc(b, &db.Y, Bs * db.Npad))) return fail(rc);
   if ((rc = dalloc(b, &db.K, Bs * db.mat))) return fail(rc);
+  if ((rc = dalloc(b, &db.Kd, Bs * db.nt * (size_t)(TS * TS)))) return fail(rc);
   if ((rc = dalloc(b, &db.Lw, Bs * db.mat))) return fail(rc);
   if ((rc = dalloc(b, &db.Linv, Bs * db.mat))) return fail(rc);
   if ((rc = dalloc(b, &db.Mt, Bs * db.mat))) return fail(rc);

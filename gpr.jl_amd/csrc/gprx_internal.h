@@ -41,7 +41,9 @@ struct DevBatch {
                                //                 dimensions d..xs-1 zero (theta-independent; the
                                //                 gradient's distance sums)
   double* Y;                   // B x Npad        (y - mean(X), zero padded)
-  double* K;                   // B x mat
+  double* K;                   // B x mat: lower tiles K (factorised in place); upper tile (j, i) = Kf tile (i, j)
+                               //   for i > j (the Gram's noise-free kernel values, read by k_lauum_grad)
+  double* Kd;                  // B x nt x 64 x 64: the Kf diagonal tiles (column-major)
   double* Lw;                  // B x mat
   double* Linv;                // B x mat
   double* Mt;                  // B x mat

@@ -367,16 +367,36 @@ __device__ __forceinline__ void mma_64x64(d4 (&acc)[QM][QN], const double* __res
 // The peeled trips carry compile-time masks; skipped products are exact zeros, so the sums are
 // bit-identical to the full core's.  Shared panels (B = A) load the fragments once.
 enum CoreMode { PLAIN = 0, TRI_A_FIRST, TRI_AB_FIRST, LOWER_SAME, TRI_A_LAST, TRI_B_LAST, REV_A, REV_B };
+// Operand addressing: element (row, k) at base[row + k ld]; lane (lr, lk) of sub-step s of stage st
+// reads k = 8 st + 4 s + lk of rows 16 a + lr (a 16-row block reads 128 contiguous bytes).
+struct CorePtr {
+  const double* p;  // this lane's address of stage 0, sub-step 0, row block 0
+  ptrdiff_t st;     // stage stride
+  ptrdiff_t sub;    // sub-step stride
+};
+__device__ __forceinline__ CorePtr core_ptr(const double* X, size_t ld) {
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  const ptrdiff_t L = (ptrdiff_t)ld;
+  return CorePtr{X + lr + lk * L, 8 * L, 4 * L};
+}
+__device__ __forceinline__ CorePtr core_rev(CorePtr c, int nst) {  // stages and sub-steps backward
+  c.p += (ptrdiff_t)(nst - 1) * c.st + c.sub;
+  c.st = -c.st;
+  c.sub = -c.sub;
+  return c;
+}
 template <int A0, int A1, int B0, int B1, bool SAME>
-__device__ __forceinline__ void frag4_load_r(Frag4& f, const double* pa, const double* pb, ptrdiff_t sa, ptrdiff_t sb) {
+__device__ __forceinline__ void frag4_load_r(Frag4& f, const CorePtr& A, const CorePtr& B, int st) {
   constexpr int L0 = SAME ? (A0 < B0 ? A0 : B0) : A0, L1 = SAME ? (A1 > B1 ? A1 : B1) : A1;
+  const double* pa = A.p + (ptrdiff_t)st * A.st;
+  const double* pb = B.p + (ptrdiff_t)st * B.st;
 #pragma unroll
   for (int s = 0; s < Q4SD; ++s) {
 #pragma unroll
-    for (int a = L0; a < L1; ++a) f.a[s][a] = pa[s * sa + 16 * a];
+    for (int a = L0; a < L1; ++a) f.a[s][a] = pa[s * A.sub + 16 * a];
     if constexpr (!SAME) {
 #pragma unroll
-      for (int b = B0; b < B1; ++b) f.b[s][b] = pb[s * sb + 16 * b];
+      for (int b = B0; b < B1; ++b) f.b[s][b] = pb[s * B.sub + 16 * b];
     }
   }
 }
@@ -403,11 +423,10 @@ struct TripMask {
   static constexpr int b1 = (!dense && MODE == TRI_AB_FIRST) ? T + 1 : QN;
 };
 template <int MODE, int T>
-__device__ __forceinline__ void core_load(Frag4& f, const double* pa, const double* pb, ptrdiff_t sa, ptrdiff_t sb,
-                                          int st) {
+__device__ __forceinline__ void core_load(Frag4& f, const CorePtr& A, const CorePtr& B, int st) {
   constexpr bool same = MODE == TRI_AB_FIRST || MODE == LOWER_SAME;
   using M = TripMask<MODE, T>;
-  frag4_load_r<M::a0, M::a1, M::b0, M::b1, same>(f, pa + (ptrdiff_t)st * Q4SD * sa, pb + (ptrdiff_t)st * Q4SD * sb, sa, sb);
+  frag4_load_r<M::a0, M::a1, M::b0, M::b1, same>(f, A, B, st);
 }
 template <int MODE, int T>
 __device__ __forceinline__ void core_mma(d4 (&acc)[QM][QN], const Frag4& f) {
@@ -415,26 +434,22 @@ __device__ __forceinline__ void core_mma(d4 (&acc)[QM][QN], const Frag4& f) {
   constexpr bool same = MODE == TRI_AB_FIRST || MODE == LOWER_SAME;
   frag4_mma_r<M::a0, M::a1, M::b0, M::b1, same, same>(acc, f);
 }
-// group barriers of a dense half trip: one load per two MFMAs (shared panels: 8 loads, 20 MFMAs)
+// group barriers of a dense half trip: its loads spread evenly over its MFMAs (one load per two
+// MFMAs; shared panels: 8 loads, 20 MFMAs)
 template <int MODE>
 __device__ __forceinline__ void core_groups() {
-  if constexpr (MODE == TRI_AB_FIRST || MODE == LOWER_SAME) {
+  constexpr bool same = MODE == TRI_AB_FIRST || MODE == LOWER_SAME;
+  constexpr int la = Q4SD * QM, lb = same ? 0 : Q4SD * QN;
+  constexpr int nl = la + lb, nm = Q4SD * (same ? 10 : QM * QN), q = nm / nl, r = nm % nl;
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
-    }
+  for (int g = 0; g < r; ++g) {
+    __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, q + 1, 0);
+  }
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-    }
-  } else {
-#pragma unroll
-    for (int g = 0; g < Q4SD * (QM + QN); ++g) {
-      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-    }
+  for (int g = r; g < nl; ++g) {
+    __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, q, 0);
   }
 }
 template <int MODE>
@@ -442,43 +457,40 @@ __device__ __forceinline__ void mma_64x64_m(d4 (&acc)[QM][QN], const double* __r
                                             const double* __restrict__ B, size_t ldb, int K) {
   const int nst = __builtin_amdgcn_readfirstlane(K / (4 * Q4SD));  // multiple of 8: K is whole 64-tiles
   if (nst <= 0) return;
-  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
-  const double* pa = A + lr + (ptrdiff_t)lk * (ptrdiff_t)lda;
-  const double* pb = B + lr + (ptrdiff_t)lk * (ptrdiff_t)ldb;
-  const ptrdiff_t sa = 4 * (ptrdiff_t)lda, sb = 4 * (ptrdiff_t)ldb;
+  const CorePtr pa = core_ptr(A, lda), pb = core_ptr(B, ldb);
   constexpr bool first = MODE == TRI_A_FIRST || MODE == TRI_AB_FIRST;
   constexpr bool last = MODE == TRI_A_LAST || MODE == TRI_B_LAST;
   Frag4 f0, f1;
   // one peeled trip T of the triangular tile, stages st and st + 1; the prefetch of stage st + 2
   // uses trip T2's masks (NX: whether there is a next stage at all)
-#define GPRX_TRIP(M, T, T2, st, NX)                       \
-  {                                                       \
-    __builtin_amdgcn_sched_barrier(0);                    \
-    core_load<M, T>(f1, pa, pb, sa, sb, (st) + 1);        \
-    core_mma<M, T>(acc, f0);                              \
-    __builtin_amdgcn_sched_barrier(0);                    \
-    if (NX) core_load<M, T2>(f0, pa, pb, sa, sb, (st) + 2); \
-    core_mma<M, T>(acc, f1);                              \
+#define GPRX_TRIP(M, T, T2, st, NX)                  \
+  {                                                  \
+    __builtin_amdgcn_sched_barrier(0);               \
+    core_load<M, T>(f1, pa, pb, (st) + 1);      \
+    core_mma<M, T>(acc, f0);                         \
+    __builtin_amdgcn_sched_barrier(0);               \
+    if (NX) core_load<M, T2>(f0, pa, pb, (st) + 2); \
+    core_mma<M, T>(acc, f1);                         \
   }
   int it = 0, end = nst;
   if constexpr (first) {
-    core_load<MODE, 0>(f0, pa, pb, sa, sb, 0);
+    core_load<MODE, 0>(f0, pa, pb, 0);
     GPRX_TRIP(MODE, 0, 1, 0, true)
     GPRX_TRIP(MODE, 1, 2, 2, true)
     GPRX_TRIP(MODE, 2, 3, 4, true)
     it = 6;
   } else {
-    core_load<MODE, last ? 0 : 4>(f0, pa, pb, sa, sb, 0);
+    core_load<MODE, last ? 0 : 4>(f0, pa, pb, 0);
     if constexpr (last) end = nst - 8;
   }
   for (; it < end; it += 2) {
     __builtin_amdgcn_sched_barrier(0);
-    core_load<MODE, 4>(f1, pa, pb, sa, sb, it + 1);
+    core_load<MODE, 4>(f1, pa, pb, it + 1);
     core_mma<MODE, 4>(acc, f0);
     core_groups<MODE>();
     __builtin_amdgcn_sched_barrier(0);
     const int n2 = (it + 2 < nst) ? it + 2 : nst - 1;
-    core_load<MODE, 4>(f0, pa, pb, sa, sb, n2);
+    core_load<MODE, 4>(f0, pa, pb, n2);
     core_mma<MODE, 4>(acc, f1);
     core_groups<MODE>();
     __builtin_amdgcn_sched_barrier(0);
@@ -503,35 +515,30 @@ __device__ __forceinline__ void mma_64x64_pm(d4 (&acc)[QM][QN], const double* __
                                              const double* __restrict__ B, size_t ldb, int K, bool tri) {
   const int nst = __builtin_amdgcn_readfirstlane(K / (4 * Q4SD));
   if (nst <= 0) return;
-  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
-  const double* pa = A + lr + (ptrdiff_t)lk * (ptrdiff_t)lda;
-  const double* pb = B + lr + (ptrdiff_t)lk * (ptrdiff_t)ldb;
-  ptrdiff_t sa = 4 * (ptrdiff_t)lda, sb = 4 * (ptrdiff_t)ldb;
+  CorePtr pa = core_ptr(A, lda), pb = core_ptr(B, ldb);
   Frag4 f0, f1;
   int it = 0;
   if (tri) {
-    if constexpr (PM == REV_A || PM == REV_B) {  // sub-step j reads k-block K/4 - 1 - j
-      pa += (ptrdiff_t)(nst * Q4SD - 1) * sa;
-      pb += (ptrdiff_t)(nst * Q4SD - 1) * sb;
-      sa = -sa;
-      sb = -sb;
+    if constexpr (PM == REV_A || PM == REV_B) {  // stage j reads the k of stage nst - 1 - j
+      pa = core_rev(pa, nst);
+      pb = core_rev(pb, nst);
     }
-    core_load<PM, 0>(f0, pa, pb, sa, sb, 0);
+    core_load<PM, 0>(f0, pa, pb, 0);
     GPRX_TRIP(PM, 0, 1, 0, true)
     GPRX_TRIP(PM, 1, 2, 2, true)
     GPRX_TRIP(PM, 2, 3, 4, true)
     it = 6;
   } else {
-    core_load<PLAIN, 4>(f0, pa, pb, sa, sb, 0);
+    core_load<PLAIN, 4>(f0, pa, pb, 0);
   }
   for (; it < nst; it += 2) {
     __builtin_amdgcn_sched_barrier(0);
-    core_load<PLAIN, 4>(f1, pa, pb, sa, sb, it + 1);
+    core_load<PLAIN, 4>(f1, pa, pb, it + 1);
     core_mma<PLAIN, 4>(acc, f0);
     core_groups<PLAIN>();
     __builtin_amdgcn_sched_barrier(0);
     const int n2 = (it + 2 < nst) ? it + 2 : nst - 1;
-    core_load<PLAIN, 4>(f0, pa, pb, sa, sb, n2);
+    core_load<PLAIN, 4>(f0, pa, pb, n2);
     core_mma<PLAIN, 4>(acc, f1);
     core_groups<PLAIN>();
     __builtin_amdgcn_sched_barrier(0);
@@ -798,20 +805,27 @@ __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
 #pragma unroll
   for (int b = 0; b < 4; ++b) {
     const int gj = j * TS + 4 * cb + b;
-    double kv[4];
+    double kv[4], fv[4];  // K and the noise-free Kf
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
       const int gi = i * TS + 4 * rb + a;
       if (gi >= db.N || gj >= db.N) {
         kv[a] = (gi == gj) ? 1.0 : 0.0;
+        fv[a] = 0.0;
       } else {
-        const double fv = sf2 * exp_k(-rr[a][b] * 0.5, ek);
-        kv[a] = (gi == gj) ? fv + noise : fv;
+        fv[a] = sf2 * exp_k(-rr[a][b] * 0.5, ek);
+        kv[a] = (gi == gj) ? fv[a] + noise : fv[a];
       }
     }
     const size_t off = (size_t)gj * db.ld + i * TS + 4 * rb;
     *(double2*)(K + off) = make_double2(kv[0], kv[1]);
     *(double2*)(K + off + 2) = make_double2(kv[2], kv[3]);
+    // the noise-free copy for the gradient epilogue: Kf tile (i, j) in the unused upper tile (j, i)
+    // (same in-tile layout), the diagonal tiles in Kd
+    double* Kc = i > j ? K + (size_t)(i * TS + 4 * cb + b) * db.ld + j * TS + 4 * rb
+                       : db.Kd + ((size_t)slot * db.nt + i) * (TS * TS) + (4 * cb + b) * TS + 4 * rb;
+    *(double2*)Kc = make_double2(fv[0], fv[1]);
+    *(double2*)(Kc + 2) = make_double2(fv[2], fv[3]);
   }
 }
 
@@ -1622,7 +1636,8 @@ __global__ __launch_bounds__(NTHR) void k_alpha(DevBatch db, int phase) {
 //   G_rc = wt_rc * (alpha_r alpha_c - Kinv_rc) * Kf_rc    (wt = 1/2 on the diagonal, as
 //                                                        dmll_kern! weights ααinvcKI[j,j]/2)
 //   S_p = sum G_rc (x_pr - x_pc)^2,  S_f = sum G_rc,  T = sum_diag W_rr
-// One gradient partial row per unit of 4 tiles.
+// One gradient partial row per unit of 4 tiles.  Kf is the Gram's own noise-free copy (upper
+// tiles of K, diagonal tiles in Kd), read once per output tile.
 //
 // The distance sums are expanded per wave tile (rows r, columns c):
 //   S_p = sum_r x_pr^2 R_r + sum_c x_pc^2 C_c - 2 sum_r x_pr Q_rp,   Q = G Xc  (64 x d)
@@ -1633,7 +1648,7 @@ __global__ __launch_bounds__(NTHR) void k_alpha(DevBatch db, int phase) {
 // removed; S_p is translation invariant), which keeps the expansion's cancellation at the
 // rounding level of the points' spread, as for the reference's own a^2 + b^2 - 2ab distances.
 // LDS: the unit's point tiles as raw [point][xs] images (LDS-DMA, issued before the MFMA loop),
-// per-wave partials, norms and alpha of the image points.
+// per-wave partials and alpha of the image points.
 // ============================================================================================
 __device__ __forceinline__ void dma_tile(double* lds, const double* src, int ndbl) {
   // ndbl doubles (even) from src to lds, 16 B per lane, one wave-instruction per KiB;
@@ -1646,11 +1661,11 @@ __device__ __forceinline__ void dma_tile(double* lds, const double* src, int ndb
   }
 }
 constexpr int SPW = DMAX + 2;  // per-wave partial row: S_p (d), S_f, T
-// LDS of a lauum workgroup: per-wave partials, the images' weighted squared norms and alpha, il2,
-// then nimg point-tile images [64][xs] (16-B aligned: the small arrays hold an even count)
-static_assert((4 * SPW + 2 * 5 * TS + DMAX) % 2 == 0, "lauum LDS image base alignment");
+// LDS of a lauum workgroup: per-wave partials, alpha of the image points, then nimg point-tile
+// images [64][xs] (16-B aligned: the small arrays hold an even count)
+static_assert((4 * SPW + 5 * TS) % 2 == 0, "lauum LDS image base alignment");
 __host__ __device__ inline size_t lauum_lds_dbl(int xs, int nimg) {
-  return (size_t)4 * SPW + 2 * 5 * TS + DMAX + (size_t)nimg * TS * xs;
+  return (size_t)4 * SPW + 5 * TS + (size_t)nimg * TS * xs;
 }
 // Unit = 4 output tiles of the lower triangle, one per wave, each with its own K range [ti, nt)
 // (register-direct operands: the waves share no panel, only the unit's point-tile images for the
@@ -1680,10 +1695,8 @@ __device__ __forceinline__ void lauum_unit(const DevBatch& db, int slot, const i
   const int xs = db.xs, xt = TS * xs;  // point-tile image: [64][xs]
   const int nimg = ju[1];
   double* sp = sm;                      // [4][SPW]
-  double* nrm = sp + 4 * SPW;           // [nimg][64] weighted squared norms of the image points
-  double* als = nrm + 5 * TS;           // [nimg][64] alpha of the same points
-  double* wl = als + 5 * TS;            // [DMAX] il2
-  double* img = wl + DMAX;              // [nimg][64][xs]
+  double* als = sp + 4 * SPW;           // [nimg][64] alpha of the image points
+  double* img = als + 5 * TS;           // [nimg][64][xs]
   const int nt = db.nt;
   const double* X = db.Xc + (size_t)slot * db.Npad * xs;
   const double* al = db.alpha + (size_t)slot * db.Npad;
@@ -1714,51 +1727,35 @@ __device__ __forceinline__ void lauum_unit(const DevBatch& db, int slot, const i
   double* spw = sp + w * SPW;
   for (int e = l; e < SPW; e += 64) spw[e] = 0.0;
   const double* P = db.params + (size_t)slot * db.pst;
-  if (tid < d) wl[tid] = P[tid];
-  for (int e = tid; e < nimg * TS; e += NTHR) {  // one image point per thread
-    const double* xp = img + (size_t)e * xs;
-    double nn = 0.0;
-    for (int p = 0; p < d; ++p) nn = fma(P[p] * xp[p], xp[p], nn);
-    nrm[e] = nn;
-    als[e] = al[ju[2 + (e >> 6)] * TS + (e & 63)];
-  }
+  for (int e = tid; e < nimg * TS; e += NTHR) als[e] = al[ju[2 + (e >> 6)] * TS + (e & 63)];
   __syncthreads();
   if (active) {
     const double sf2 = P[d];
     const int ir = ju[15 + w], ic = ju[19 + w];
     const double* xr = img + ir * xt;  // [r][xs]
     const double* xc = img + ic * xt;  // [c][xs]
-    const double* nr = nrm + ir * TS;
-    const double* nc = nrm + ic * TS;
     const double* ar = als + ir * TS;
     const double* ac = als + ic * TS;
-    const int KS = (d + 3) >> 2;
-    const ExpK ek = g_expk;
-    // G in place of acc:  Kf recomputed from r = n_r + n_c - 2 sum_p il2_p xc_pr xc_pc (MFMA, one
-    // 16 x 16 block at a time; the same centred points as the distance sums below)
+    // G in place of acc, with Kf read back from the Gram's noise-free copy (upper tile (tj, ti) of K,
+    // or Kd for a diagonal tile): the same kernel values the factorisation used
+    const double* Kf;
+    size_t ldk;
+    if (ti == tj) {
+      Kf = db.Kd + ((size_t)slot * nt + ti) * (TS * TS);
+      ldk = TS;
+    } else {
+      Kf = db.K + so + (size_t)(ti * TS) * ld + tj * TS;
+      ldk = ld;
+    }
 #pragma unroll
     for (int a = 0; a < QM; ++a) {
-      // cross terms of row block a against the 4 column blocks: 4 independent MFMA chains over
-      // the (unrolled, predicated) dimension steps, so the LDS operand loads of the next step
-      // overlap the current step's MFMAs
-      d4 cr4[QN];
+      double kf[QN][4];
 #pragma unroll
-      for (int b = 0; b < QN; ++b) cr4[b] = (d4){0.0, 0.0, 0.0, 0.0};
+      for (int b = 0; b < QN; ++b)
 #pragma unroll
-      for (int s2 = 0; s2 < (DMAX + 3) / 4; ++s2) {
-        if (s2 < KS) {
-          // dimensions k >= d (the last step's padding): the A operand is zero, the B operand a
-          // finite image value (clamped index)
-          const int k = 4 * s2 + lk, kc = k < d ? k : d - 1;
-          const double xv = wl[kc] * xr[(16 * a + lr) * xs + kc];
-          const double xa = k < d ? xv : 0.0;
-#pragma unroll
-          for (int b = 0; b < QN; ++b) cr4[b] = mfma(xc[(16 * b + lr) * xs + kc], xa, cr4[b]);
-        }
-      }
+        for (int q = 0; q < 4; ++q) kf[b][q] = Kf[(size_t)(16 * b + lk + 4 * q) * ldk + 16 * a + lr];
 #pragma unroll
       for (int b = 0; b < QN; ++b) {
-        const d4 cr = cr4[b];  // cr[q] = sum_p il2 x_{p,16a+lr} x_{p,16b+lk+4q}
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int r = 16 * a + lr, c = 16 * b + lk + 4 * q;
@@ -1770,9 +1767,7 @@ __device__ __forceinline__ void lauum_unit(const DevBatch& db, int slot, const i
               G = 0.5 * (W * sf2);
               tr += W;
             } else {
-              const double rr = fma(-2.0, cr[q], nr[r] + nc[c]);
-              const double kf = sf2 * exp_k(-0.5 * (rr > 0.0 ? rr : 0.0), ek);
-              G = W * kf;
+              G = W * kf[b][q];
             }
             sf += G;
           }
