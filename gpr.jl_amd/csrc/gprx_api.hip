@@ -267,14 +267,15 @@ void predict_group(gprx_ctx* c, hipStream_t st, const DevBatch& db) {
 // Whole evaluation of a batch (or a slot range of it) on stream `st`.
 void eval_group(gprx_ctx* c, hipStream_t st, const DevBatch& db, bool want_grad, bool want_pred) {
   const double Bd = db.B, nt = db.nt, Np = db.Npad, d = db.d;
-  timed(c, st, "gram", Bd * 3.0 * db.N * (double)db.N * d / 2.0, Bd * 8.0 * (Np * Np / 2.0 + Np * d),
+  // bytes: the lower tiles of K and the noise-free copy for the gradient written, X read
+  timed(c, st, "gram", Bd * 3.0 * db.N * (double)db.N * d / 2.0, Bd * 8.0 * (Np * Np + Np * d),
         [&] { gprx::launch_gram(db, st); });
   factor_rec(c, st, db, 0, db.nt);
   timed(c, st, "alpha", Bd * Np * nt, Bd * 8.0 * Np * nt, [&] { gprx::launch_alpha(db, st, 0); });
   timed(c, st, "alpha", Bd * Np * Np, Bd * 8.0 * Np * Np / 2.0, [&] { gprx::launch_alpha(db, st, 1); });
   if (want_grad)
-    timed(c, st, "lauum_grad", Bd * (Np * Np * Np / 3.0 + 2.0 * Np * Np * d + 4.0 * Np * Np),
-          Bd * 8.0 * (Np * Np / 2.0 + Np * (db.xs + 2.0)),  // minimum: Mt upper, Xc, alpha once
+    timed(c, st, "lauum_grad", Bd * (Np * Np * Np / 3.0 + Np * Np * d + 4.0 * Np * Np),
+          Bd * 8.0 * (Np * Np + Np * (db.xs + 2.0)),  // minimum: Mt upper, Kf lower, Xc, alpha once
           [&] { gprx::launch_lauum_grad(db, st); });
   timed(c, st, "finalize", Bd * 2.0 * db.N, Bd * 16.0 * db.N, [&] { gprx::launch_finalize(db, want_grad ? 1 : 0, st); });
   if (want_pred) predict_group(c, st, db);
