@@ -113,8 +113,7 @@ def pmc_field(stat: str, global_batch: int, fields):
 
 def roofline_parts(kern: dict, nprof: int, global_batch: int) -> dict:
     """The north star's two roofline figures beside the dominant kernel's: the Gram build against
-    HBM (algorithmic bytes 8 (Npad^2 + Npad d) per slot: the lower tiles of K and the noise-free
-    copy the gradient reads written, X read)
+    HBM (algorithmic bytes 8 (Npad^2/2 + Npad d) per slot: the lower tiles of K written, X read)
     and the whole factorisation (leaf + TRSM + SYRK/TT + LINV21: Cholesky and L^-1, N^3/3 + N^3/3
     flops per slot) against the fp64 MFMA peak; the prediction-variance GEMM too.  Achieved =
     algorithmic work / HIP-event time on the library stream, per launch."""

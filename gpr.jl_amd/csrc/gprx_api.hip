@@ -210,33 +210,35 @@ int copy_in(gprx_ctx* c, void* dst, const void* src, size_t bytes, int mem) {
 }
 
 // Recursive Cholesky + inverse over tile range [o, o+n) (tile units), all slots in lock step.
-void factor_rec(gprx_ctx* c, hipStream_t st, const DevBatch& db, int o, int n) {
+// upd: the node lies in the trailing block of an ancestor (its tiles were updated into S); the top
+// child inherits the parent's flag, the bottom child follows the parent's SYRK
+void factor_rec(gprx_ctx* c, hipStream_t st, const DevBatch& db, int o, int n, int upd) {
   const double T = TS, Bd = db.B;
   const int leaf = c->leaf_tiles > 0 ? c->leaf_tiles : (db.B >= 32 ? 4 : 1);
   if (n > 1 && n <= leaf) {
     const double m = n * T;
     timed(c, st, "leaf", Bd * (m * m * m / 3.0 + m * m * m / 3.0), Bd * 8.0 * 3.0 * m * m,
-          [&] { gprx::launch_leaf(db, o, n, st); }, n);
+          [&] { gprx::launch_leaf(db, o, n, upd, st); }, n);
     return;
   }
   if (n == 1) {
     timed(c, st, "diag", Bd * (T * T * T / 3.0 + T * T * T / 3.0), Bd * 8.0 * 3.0 * T * T,
-          [&] { gprx::launch_diag(db, o, st); });
+          [&] { gprx::launch_diag(db, o, upd, st); });
     return;
   }
   const int h = n / 2;
   const double m1 = h * T, m2 = (n - h) * T;
-  factor_rec(c, st, db, o, h);
-  gprx::GemmGeom g{gprx::OP_TRSM, o, h, n};
+  factor_rec(c, st, db, o, h, upd);
+  gprx::GemmGeom g{gprx::OP_TRSM, o, h, n, upd};
   const double f_trsm = Bd * m2 * m1 * m1, f_syrk = Bd * m2 * m2 * m1, f_tt = Bd * m2 * m1 * m1,
                f_linv = Bd * m1 * m2 * m2;
   const double b_trsm = Bd * 8.0 * (2.0 * m2 * m1 + m1 * m1 / 2.0), b_syrk = Bd * 8.0 * (m2 * m1 + m2 * m2),
                b_tt = Bd * 8.0 * (2.0 * m2 * m1 + m1 * m1 / 2.0), b_linv = Bd * 8.0 * (3.0 * m2 * m1 + m2 * m2 / 2.0);
   timed(c, st, "potrf_trsm", f_trsm, b_trsm, [&] { gprx::launch_gemm(db, g, st); }, n);
-  gprx::GemmGeom gs{gprx::OP_SYRK, o, h, n}, gt{gprx::OP_TT, o, h, n};
+  gprx::GemmGeom gs{gprx::OP_SYRK, o, h, n, upd}, gt{gprx::OP_TT, o, h, n, upd};
   // T^T = L11^-T L21^T needs only rec(A11) and the TRSM: it runs in the SYRK's launch
   timed(c, st, "syrk_tt", f_syrk + f_tt, b_syrk + b_tt, [&] { gprx::launch_gemm(db, gs, st, gt); }, n);
-  factor_rec(c, st, db, o + h, n - h);
+  factor_rec(c, st, db, o + h, n - h, 1);
   g.op = gprx::OP_LINV21;
   timed(c, st, "trtri_linv21", f_linv, b_linv, [&] { gprx::launch_gemm(db, g, st); }, n);
 }
@@ -267,10 +269,9 @@ void predict_group(gprx_ctx* c, hipStream_t st, const DevBatch& db) {
 // Whole evaluation of a batch (or a slot range of it) on stream `st`.
 void eval_group(gprx_ctx* c, hipStream_t st, const DevBatch& db, bool want_grad, bool want_pred) {
   const double Bd = db.B, nt = db.nt, Np = db.Npad, d = db.d;
-  // bytes: the lower tiles of K and the noise-free copy for the gradient written, X read
-  timed(c, st, "gram", Bd * 3.0 * db.N * (double)db.N * d / 2.0, Bd * 8.0 * (Np * Np + Np * d),
+  timed(c, st, "gram", Bd * 3.0 * db.N * (double)db.N * d / 2.0, Bd * 8.0 * (Np * Np / 2.0 + Np * d),
         [&] { gprx::launch_gram(db, st); });
-  factor_rec(c, st, db, 0, db.nt);
+  factor_rec(c, st, db, 0, db.nt, 0);
   timed(c, st, "alpha", Bd * Np * nt, Bd * 8.0 * Np * nt, [&] { gprx::launch_alpha(db, st, 0); });
   timed(c, st, "alpha", Bd * Np * Np, Bd * 8.0 * Np * Np / 2.0, [&] { gprx::launch_alpha(db, st, 1); });
   if (want_grad)
@@ -482,7 +483,7 @@ int gprx_batch_create(gprx_ctx* c, int B, int d, int N, int M_max, gprx_batch** 
   if ((rc = dalloc(b, &db.Xc, Bs * db.Npad * db.xs))) return fail(rc);
   if ((rc = dalloc(b, &db.Y, Bs * db.Npad))) return fail(rc);
   if ((rc = dalloc(b, &db.K, Bs * db.mat))) return fail(rc);
-  if ((rc = dalloc(b, &db.Kd, Bs * db.nt * (size_t)(TS * TS)))) return fail(rc);
+  if ((rc = dalloc(b, &db.S, Bs * db.mat))) return fail(rc);
   if ((rc = dalloc(b, &db.Lw, Bs * db.mat))) return fail(rc);
   if ((rc = dalloc(b, &db.Linv, Bs * db.mat))) return fail(rc);
   if ((rc = dalloc(b, &db.Mt, Bs * db.mat))) return fail(rc);
@@ -517,7 +518,8 @@ int gprx_batch_create(gprx_ctx* c, int B, int d, int N, int M_max, gprx_batch** 
       hipMemset(db.Y, 0, Bs * db.Npad * sizeof(double)) != hipSuccess ||
       hipMemset(db.Lw, 0, Bs * db.mat * sizeof(double)) != hipSuccess ||
       hipMemset(db.Linv, 0, Bs * db.mat * sizeof(double)) != hipSuccess ||
-      hipMemset(db.Mt, 0, Bs * db.mat * sizeof(double)) != hipSuccess)
+      hipMemset(db.Mt, 0, Bs * db.mat * sizeof(double)) != hipSuccess ||
+      hipMemset(db.S, 0, Bs * db.mat * sizeof(double)) != hipSuccess)
     return fail(GPRX_DEVICE_ERROR);
   *out = b;
   return GPRX_OK;

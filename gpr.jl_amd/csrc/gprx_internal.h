@@ -41,9 +41,9 @@ struct DevBatch {
                                //                 dimensions d..xs-1 zero (theta-independent; the
                                //                 gradient's distance sums)
   double* Y;                   // B x Npad        (y - mean(X), zero padded)
-  double* K;                   // B x mat: lower tiles K (factorised in place); upper tile (j, i) = Kf tile (i, j)
-                               //   for i > j (the Gram's noise-free kernel values, read by k_lauum_grad)
-  double* Kd;                  // B x nt x 64 x 64: the Kf diagonal tiles (column-major)
+  double* K;                   // B x mat: lower tiles of K as the Gram wrote them (kept: the gradient
+                               //   reads its off-diagonal entries as Kf)
+  double* S;                   // B x mat: lower tiles of the trailing matrices the SYRKs update
   double* Lw;                  // B x mat
   double* Linv;                // B x mat
   double* Mt;                  // B x mat
@@ -83,6 +83,7 @@ constexpr int OP_NONE = -1;
 struct GemmGeom {
   int op;
   int o, h, n;  // node: offset o, split h, size n (tile units); block1 = [o, o+h), block2 = [o+h, o+n)
+  int upd = 0;  // the node lies in an ancestor's trailing block: its tiles are read from S, not K
 };
 // Output rectangle of an op in tiles: origin (r0, c0), R x C, lower triangle only when tri.
 __host__ __device__ inline void op_rect(const GemmGeom& g, int nt, int mt, int& r0, int& c0, int& R, int& C, bool& tri) {
@@ -209,8 +210,8 @@ size_t lbfgs_lds_bytes(int n, int m);
 void launch_params(const DevBatch& b, hipStream_t s);
 void launch_gram(const DevBatch& b, hipStream_t s);
 void launch_center(const DevBatch& b, hipStream_t s);
-void launch_diag(const DevBatch& b, int jt, hipStream_t s);
-void launch_leaf(const DevBatch& b, int o, int n, hipStream_t s);
+void launch_diag(const DevBatch& b, int jt, int upd, hipStream_t s);
+void launch_leaf(const DevBatch& b, int o, int n, int upd, hipStream_t s);
 // one launch; with g2.op != OP_NONE the units of g2 are appended to g's (independent ops)
 void launch_gemm(const DevBatch& b, const GemmGeom& g, hipStream_t s, const GemmGeom& g2 = GemmGeom{OP_NONE, 0, 0, 0});
 void launch_alpha(const DevBatch& b, hipStream_t s, int phase);

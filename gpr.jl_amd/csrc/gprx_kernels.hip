@@ -805,27 +805,20 @@ __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
 #pragma unroll
   for (int b = 0; b < 4; ++b) {
     const int gj = j * TS + 4 * cb + b;
-    double kv[4], fv[4];  // K and the noise-free Kf
+    double kv[4];
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
       const int gi = i * TS + 4 * rb + a;
       if (gi >= db.N || gj >= db.N) {
         kv[a] = (gi == gj) ? 1.0 : 0.0;
-        fv[a] = 0.0;
       } else {
-        fv[a] = sf2 * exp_k(-rr[a][b] * 0.5, ek);
-        kv[a] = (gi == gj) ? fv[a] + noise : fv[a];
+        const double fv = sf2 * exp_k(-rr[a][b] * 0.5, ek);
+        kv[a] = (gi == gj) ? fv + noise : fv;
       }
     }
     const size_t off = (size_t)gj * db.ld + i * TS + 4 * rb;
     *(double2*)(K + off) = make_double2(kv[0], kv[1]);
     *(double2*)(K + off + 2) = make_double2(kv[2], kv[3]);
-    // the noise-free copy for the gradient epilogue: Kf tile (i, j) in the unused upper tile (j, i)
-    // (same in-tile layout), the diagonal tiles in Kd
-    double* Kc = i > j ? K + (size_t)(i * TS + 4 * cb + b) * db.ld + j * TS + 4 * rb
-                       : db.Kd + ((size_t)slot * db.nt + i) * (TS * TS) + (4 * cb + b) * TS + 4 * rb;
-    *(double2*)Kc = make_double2(fv[0], fv[1]);
-    *(double2*)(Kc + 2) = make_double2(fv[2], fv[3]);
   }
 }
 
@@ -874,19 +867,20 @@ __global__ __launch_bounds__(NTHR) void k_center(DevBatch db) {
 constexpr int FS = TS + 1;  // LDS column stride of the tile images
 // LDS of the diagonal routine (the caller's): T[c*FS + r] = A[r][c], then L (lower); Xi[c*FS + r]
 // = X[r][c] = (L^-1)[r][c] (the inverse stays there until the next call); cbs: [256] scratch.
-// t_ready: T already holds the tile's lower triangle (zeros above), written by the caller.
+// t_ready: T already holds the tile's lower triangle (zeros above), written by the caller; else
+// it is read from Ksrc (K, or S when a SYRK updated it).
 __device__ __forceinline__ void diag_tile_fast(const DevBatch& db, int slot, int jt, double* T, double* Xi, double* cbs,
-                                               bool t_ready);
-__global__ __launch_bounds__(NTHR) void k_diag_f(DevBatch db, int jt) {
+                                               bool t_ready, const double* Ksrc);
+__global__ __launch_bounds__(NTHR) void k_diag_f(DevBatch db, int jt, int upd) {
   __shared__ double T[TS * FS], Xi[TS * FS];
   __shared__ __attribute__((aligned(16))) double cbs[256];
-  if (slot_active(db, blockIdx.x)) diag_tile_fast(db, blockIdx.x, jt, T, Xi, cbs, false);
+  if (slot_active(db, blockIdx.x)) diag_tile_fast(db, blockIdx.x, jt, T, Xi, cbs, false, upd ? db.S : db.K);
 }
 __device__ __forceinline__ void diag_tile_fast(const DevBatch& db, int slot, int jt, double* T, double* Xi, double* cbs,
-                                               bool t_ready) {
+                                               bool t_ready, const double* Ksrc) {
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, lr = l & 15, lk = l >> 4;
   const size_t ld = db.ld;
-  const double* A = db.K + (size_t)slot * db.mat + (size_t)jt * TS * ld + jt * TS;
+  const double* A = Ksrc + (size_t)slot * db.mat + (size_t)jt * TS * ld + jt * TS;
   for (int e = tid; e < TS * TS; e += NTHR) {
     const int r = e & 63, c = e >> 6;
     if (!t_ready) T[c * FS + r] = (r >= c) ? A[(size_t)c * ld + r] : 0.0;
@@ -1070,7 +1064,7 @@ __device__ __forceinline__ void gemm_tile(const DevBatch& db, const GemmGeom& g,
   const double *A, *Bm;
   size_t ldb = ld;
   switch (op) {
-    case OP_TRSM: kb = g.o; ke = tj + 1; A = db.K + so; Bm = db.Linv + so; break;
+    case OP_TRSM: kb = g.o; ke = tj + 1; A = (g.upd ? db.S : db.K) + so; Bm = db.Linv + so; break;
     case OP_SYRK: kb = g.o; ke = g.o + g.h; A = db.Lw + so; Bm = db.Lw + so; break;
     case OP_TT: kb = ti; ke = g.o + g.h; A = db.Mt + so; Bm = db.Lw + so; break;
     case OP_LINV21: kb = g.o + g.h; ke = ti + 1; A = db.Linv + so; Bm = db.Lw + so; break;
@@ -1085,7 +1079,7 @@ __device__ __forceinline__ void gemm_tile(const DevBatch& db, const GemmGeom& g,
   const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
   d4 acc[QM][QN];
   if (op == OP_SYRK) {  // acc = -C, loaded before the K loop so its latency overlaps the first stage
-    const double* Cs = db.K + so + (size_t)(tj * TS) * ld + ti * TS;
+    const double* Cs = (g.upd ? db.S : db.K) + so + (size_t)(tj * TS) * ld + ti * TS;
 #pragma unroll
     for (int a = 0; a < QM; ++a)
 #pragma unroll
@@ -1139,7 +1133,7 @@ __device__ __forceinline__ void gemm_tile(const DevBatch& db, const GemmGeom& g,
   double sgn = 1.0;
   switch (op) {
     case OP_TRSM: Cm = db.Lw + so; break;
-    case OP_SYRK: Cm = db.K + so; break;
+    case OP_SYRK: Cm = db.S + so; break;
     case OP_TT: Cm = db.Lw + so; break;
     default: Cm = db.Linv + so; sgn = -1.0; break;
   }
@@ -1316,7 +1310,7 @@ __device__ __forceinline__ void gemm_tile_pair(const DevBatch& db, const GemmGeo
   const double *A, *Bm;
   size_t ldb = ld;
   switch (op) {
-    case OP_TRSM: kb = g.o; ke = tj + 1; A = db.K + so; Bm = db.Linv + so; break;
+    case OP_TRSM: kb = g.o; ke = tj + 1; A = (g.upd ? db.S : db.K) + so; Bm = db.Linv + so; break;
     case OP_SYRK: kb = g.o; ke = g.o + g.h; A = db.Lw + so; Bm = db.Lw + so; break;
     case OP_TT: kb = ti; ke = g.o + g.h; A = db.Mt + so; Bm = db.Lw + so; break;
     case OP_LINV21: kb = g.o + g.h; ke = ti + 1; A = db.Linv + so; Bm = db.Lw + so; break;
@@ -1354,21 +1348,31 @@ __device__ __forceinline__ void gemm_tile_pair(const DevBatch& db, const GemmGeo
   double sgn = 1.0;
   switch (op) {
     case OP_TRSM: Cm = db.Lw + so; break;
-    case OP_SYRK: Cm = db.K + so; break;
+    case OP_SYRK: Cm = db.S + so; break;
     case OP_TT: Cm = db.Lw + so; break;
     default: Cm = db.Linv + so; sgn = -1.0; break;
   }
-  double* Ct = Cm + (size_t)(tj * TS + 32 * wc) * ld + ti * TS;
+  const size_t co = (size_t)(tj * TS + 32 * wc) * ld + ti * TS;
+  double* Ct = Cm + co;
+  if (op == OP_SYRK) {  // C (from K, or S once updated) - L L^T into S
+    const double* Cs = (g.upd ? db.S : db.K) + so + co;
 #pragma unroll
-  for (int a = 0; a < WM; ++a)
+    for (int a = 0; a < WM; ++a)
 #pragma unroll
-    for (int b = 0; b < WN; ++b)
+      for (int b = 0; b < WN; ++b)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        double* p = Ct + (size_t)(16 * b + lk + 4 * q) * ld + 16 * a + lr;
-        if (op == OP_SYRK) *p = *p - acc[a][b][q];
-        else *p = sgn * acc[a][b][q];
-      }
+        for (int q = 0; q < 4; ++q) {
+          const size_t e = (size_t)(16 * b + lk + 4 * q) * ld + 16 * a + lr;
+          Ct[e] = Cs[e] - acc[a][b][q];
+        }
+  } else {
+#pragma unroll
+    for (int a = 0; a < WM; ++a)
+#pragma unroll
+      for (int b = 0; b < WN; ++b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Ct[(size_t)(16 * b + lk + 4 * q) * ld + 16 * a + lr] = sgn * acc[a][b][q];
+  }
   if (op == OP_LINV21) zp_acc2(db, slot, ti, tj, wc, acc, -1.0);
   if (op == OP_LINV21) {  // Mt[tj, ti] = Linv[ti, tj]^T (direct: an LDS transpose measured slower here)
     double* Mtt = db.Mt + so + (size_t)(ti * TS) * ld + tj * TS + 32 * wc;
@@ -1427,7 +1431,7 @@ __device__ __forceinline__ void accq_store_t(double* Ct, size_t ld, const d4 (&a
   __builtin_amdgcn_wave_barrier();
 }
 
-__device__ __forceinline__ void leaf_body(const DevBatch& db, int o, int n) {
+__device__ __forceinline__ void leaf_body(const DevBatch& db, int o, int n, int upd) {
   // every 64 x 64 tile task is split into four 64 x 16 column quarters, one per wave (wave w:
   // columns 16w..16w+15 of every tile of a step), so a step with fewer tiles than waves keeps
   // all four SIMDs busy; quarter-transposed stores through the wave's LDS buffer
@@ -1440,7 +1444,10 @@ __device__ __forceinline__ void leaf_body(const DevBatch& db, int o, int n) {
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), cq = 16 * w;
   double* tb = tbs + w * 16 * (TS + 1);
   const size_t ld = db.ld, so = (size_t)slot * db.mat;
-  double* K = db.K + so;
+  // the leaf's tiles: from K (or S, upd) in step 0; every later step reads what this leaf's own
+  // SYRK wrote to S
+  double* S = db.S + so;
+  const double* K0 = (upd ? db.S : db.K) + so;
   double* Lw = db.Lw + so;
   double* Li = db.Linv + so;
   double* Mt = db.Mt + so;
@@ -1448,7 +1455,8 @@ __device__ __forceinline__ void leaf_body(const DevBatch& db, int o, int n) {
   for (int k = 0; k < n; ++k) {
     const int tk = o + k, m = n - 1 - k;
     const double* xi = dXi;  // Linv[tk,tk] in LDS, read by the TRSM tasks below
-    diag_tile_fast(db, slot, tk, dT, dXi, dcb, k > 0);  // k > 0: the SYRK below left the tile in dT
+    const double* K = k > 0 ? S : K0;
+    diag_tile_fast(db, slot, tk, dT, dXi, dcb, k > 0, upd ? db.S : db.K);  // k > 0: the SYRK below left the tile in dT
     __syncthreads();
     for (int t = 0; t < m; ++t) {  // TRSM: L[ti,tk] = K[ti,tk] Linv[tk,tk]^T
       const int ti = tk + 1 + t;
@@ -1462,12 +1470,13 @@ __device__ __forceinline__ void leaf_body(const DevBatch& db, int o, int n) {
     for (int c = 0; c < m; ++c)  // SYRK (lower trailing tiles)
       for (int a0 = 0; a0 < m - c; ++a0) {
         const int tj = tk + 1 + c, ti = tj + a0;
-        double* Ct = K + (size_t)(tj * TS + cq) * ld + ti * TS;
+        const double* Cs = K + (size_t)(tj * TS + cq) * ld + ti * TS;
+        double* Ct = S + (size_t)(tj * TS + cq) * ld + ti * TS;
         d4 acc[QM];  // -C - L L^T, stored negated
 #pragma unroll
         for (int a = 0; a < QM; ++a)
 #pragma unroll
-          for (int q = 0; q < 4; ++q) acc[a][q] = -Ct[(size_t)(lk + 4 * q) * ld + 16 * a + lr];
+          for (int q = 0; q < 4; ++q) acc[a][q] = -Cs[(size_t)(lk + 4 * q) * ld + 16 * a + lr];
         mma_64x16(acc, Lw + (size_t)tk * TS * ld + ti * TS, ld, Lw + (size_t)tk * TS * ld + tj * TS + cq, ld, TS);
         if (c == 0 && a0 == 0) {  // the next diagonal tile: straight into the diagonal routine's LDS
 #pragma unroll
@@ -1576,7 +1585,7 @@ __device__ __forceinline__ void leaf_body(const DevBatch& db, int o, int n) {
   }
 }
 
-__global__ __launch_bounds__(NTHR) void k_leaf(DevBatch db, int o, int n) { leaf_body(db, o, n); }
+__global__ __launch_bounds__(NTHR) void k_leaf(DevBatch db, int o, int n, int upd) { leaf_body(db, o, n, upd); }
 
 // ============================================================================================
 // alpha = L^-T (L^-1 y).  phase 0: z = Linv y ; phase 1: alpha = Mt z.   grid = B * nt
@@ -1738,15 +1747,8 @@ __device__ __forceinline__ void lauum_unit(const DevBatch& db, int slot, const i
     const double* ac = als + ic * TS;
     // G in place of acc, with Kf read back from the Gram's noise-free copy (upper tile (tj, ti) of K,
     // or Kd for a diagonal tile): the same kernel values the factorisation used
-    const double* Kf;
-    size_t ldk;
-    if (ti == tj) {
-      Kf = db.Kd + ((size_t)slot * nt + ti) * (TS * TS);
-      ldk = TS;
-    } else {
-      Kf = db.K + so + (size_t)(ti * TS) * ld + tj * TS;
-      ldk = ld;
-    }
+    const double* Kf = db.K + so + (size_t)(tj * TS) * ld + ti * TS;
+    const size_t ldk = ld;
 #pragma unroll
     for (int a = 0; a < QM; ++a) {
       double kf[QN][4];
@@ -2232,11 +2234,11 @@ __global__ __launch_bounds__(64) void k_params(DevBatch b) {
 }
 void launch_params(const DevBatch& b, hipStream_t s) { hipLaunchKernelGGL(k_params, dim3((b.B + 63) / 64), dim3(64), 0, s, b); }
 void launch_center(const DevBatch& b, hipStream_t s) { hipLaunchKernelGGL(k_center, dim3(b.B), dim3(NTHR), 0, s, b); }
-void launch_diag(const DevBatch& b, int jt, hipStream_t s) {
-  hipLaunchKernelGGL(k_diag_f, dim3(b.B), dim3(NTHR), 0, s, b, jt);
+void launch_diag(const DevBatch& b, int jt, int upd, hipStream_t s) {
+  hipLaunchKernelGGL(k_diag_f, dim3(b.B), dim3(NTHR), 0, s, b, jt, upd);
 }
-void launch_leaf(const DevBatch& b, int o, int n, hipStream_t s) {
-  hipLaunchKernelGGL(k_leaf, dim3(b.B), dim3(NTHR), 0, s, b, o, n);
+void launch_leaf(const DevBatch& b, int o, int n, int upd, hipStream_t s) {
+  hipLaunchKernelGGL(k_leaf, dim3(b.B), dim3(NTHR), 0, s, b, o, n, upd);
 }
 void launch_gemm(const DevBatch& b, const GemmGeom& g, hipStream_t s, const GemmGeom& g2) {
   if (g.op != OP_PREDVAR && g.n <= b.small_n) {  // small node: pair units, 64 x 32 waves
