@@ -624,7 +624,7 @@ __device__ __forceinline__ void mma_64x16_ldsb(d4 (&acc)[QM], const double* __re
 // (100 MHz) before and after, per wave, into a buffer no other code reads.  Not in the product build.
 #ifdef GPRX_STAMPS
 constexpr int STAMP_MAX = 1 << 18;  // waves per stamp region
-__device__ unsigned long long g_stamps[2][STAMP_MAX][4];
+__device__ unsigned long long g_stamps[3][STAMP_MAX][4];
 struct Stamp {
   unsigned long long t, r;
 };
@@ -644,6 +644,17 @@ __device__ __forceinline__ void stamp_store(int region, const Stamp& a, const St
     g_stamps[region][i][3] = b.r;
   }
 }
+// leaf timeline: s_memrealtime of wave 0 at event ev of leaf o / 4 of this slot (slots < 256)
+__device__ __forceinline__ void leaf_ts(int o, int slot, int ev) {
+  if (threadIdx.x == 0 && slot < 256) {
+    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    (&g_stamps[2][0][0])[((size_t)((o >> 2) & 7) * 256 + slot) * 32 + ev] = t;
+  }
+}
+#define LEAF_TS(ev) leaf_ts(o, slot, ev)
+#else
+#define LEAF_TS(ev)
 #endif
 __device__ __forceinline__ void acc4_zero(d4 (&acc)[QM][QN]) {
 #pragma unroll
@@ -1452,12 +1463,14 @@ __device__ __forceinline__ void leaf_body(const DevBatch& db, int o, int n, int 
   double* Li = db.Linv + so;
   double* Mt = db.Mt + so;
   const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  LEAF_TS(0);
   for (int k = 0; k < n; ++k) {
     const int tk = o + k, m = n - 1 - k;
     const double* xi = dXi;  // Linv[tk,tk] in LDS, read by the TRSM tasks below
     const double* K = k > 0 ? S : K0;
     diag_tile_fast(db, slot, tk, dT, dXi, dcb, k > 0, upd ? db.S : db.K);  // k > 0: the SYRK below left the tile in dT
     __syncthreads();
+    LEAF_TS(1 + 3 * k);
     for (int t = 0; t < m; ++t) {  // TRSM: L[ti,tk] = K[ti,tk] Linv[tk,tk]^T
       const int ti = tk + 1 + t;
       d4 acc[QM];
@@ -1467,6 +1480,7 @@ __device__ __forceinline__ void leaf_body(const DevBatch& db, int o, int n, int 
       accq_store(Lw + (size_t)(tk * TS + cq) * ld + ti * TS, ld, acc, 1.0);
     }
     __syncthreads();
+    LEAF_TS(2 + 3 * k);
     for (int c = 0; c < m; ++c)  // SYRK (lower trailing tiles)
       for (int a0 = 0; a0 < m - c; ++a0) {
         const int tj = tk + 1 + c, ti = tj + a0;
@@ -1491,6 +1505,7 @@ __device__ __forceinline__ void leaf_body(const DevBatch& db, int o, int n, int 
         }
       }
     __syncthreads();
+    LEAF_TS(3 + 3 * k);
   }
   // off-diagonal inverse tiles by sub-diagonal s:  X = sum_{k=tj}^{ti-1} L[ti,k] Linv[k,tj] (kept
   // transposed in the wave's LDS buffer), Linv[ti,tj] = -Linv[ti,ti] X.  Wave w's quarter of
@@ -1534,6 +1549,7 @@ __device__ __forceinline__ void leaf_body(const DevBatch& db, int o, int n, int 
       accq_store_t(Xt + cq, ld, acc, -1.0, tb);
     }
     __syncthreads();
+    LEAF_TS(12 + s);
   }
   // z partials of the off-diagonal L^-1 tiles of this leaf (the diagonal tiles' come from
   // diag_tile_fast).  n <= 4: the four quarters' partials from zq, summed in wave order.
@@ -1549,6 +1565,7 @@ __device__ __forceinline__ void leaf_body(const DevBatch& db, int o, int n, int 
       zp_row(db, slot, 2 * tj)[ti * TS + r] = ((zq[k][0][r] + zq[k][1][r]) + zq[k][2][r]) + zq[k][3][r];
       zp_row(db, slot, 2 * tj + 1)[ti * TS + r] = 0.0;
     }
+    LEAF_TS(16);
     return;
   }
   // larger leaves: read the tiles back from L2 (this workgroup wrote them); 16 tiles per round
