@@ -1180,58 +1180,88 @@ __device__ __forceinline__ void gemm_tile(const DevBatch& db, const GemmGeom& g,
   }
 }
 
+// The SYRK + TT launch of an 8-tile node (m1 = m2 = 4 tiles): 10 SYRK tiles of K = 4 tiles and 16 TT
+// tiles of K = 4 - i (row i), 80 tile-K in all.  The unit decomposition below gives 5 workgroups
+// per slot (1200 at B = 240: 2.34 rounds of 512 resident workgroups, i.e. three); this fixed plan
+// packs them into 2 workgroups per slot, every wave a list of 3-4 tiles summing to 10 tile-K (one
+// round).  Entry: sel * 16 + 4 i + j, tile (i, j) of the SYRK (sel 0) or TT (sel 1) rectangle.
+__constant__ int N8_PLAN[8][4] = {{0, 4, 24, -1},  {5, 8, 25, -1},  {9, 10, 26, -1},  {12, 13, 27, -1},
+                                   {14, 20, 21, -1}, {15, 22, 23, -1}, {16, 17, 28, 29}, {18, 19, 30, 31}};
+__host__ __device__ inline bool n8_plan(const GemmGeom& g1, const GemmGeom& g2) {
+  return g1.op == OP_SYRK && g2.op == OP_TT && g1.n == 8 && g1.h == 4;
+}
 template <bool PV, int PM = PLAIN>
 __device__ __forceinline__ void gemm_body(const DevBatch& db, const GemmGeom& g1, const GemmGeom& g2) {
   int r0, c0, R, C, r02, c02, R2, C2;
   bool tri, tri2;
   op_rect(g1, db.nt, db.mt, r0, c0, R, C, tri);
   op_rect(g2, db.nt, db.mt, r02, c02, R2, C2, tri2);
-  const int T1 = op_units(g1, db.nt, db.mt), T2 = g2.op == OP_NONE ? 0 : op_units(g2, db.nt, db.mt);
+  const bool plan = !PV && n8_plan(g1, g2);
+  const int T1 = plan ? 2 : op_units(g1, db.nt, db.mt), T2 = (plan || g2.op == OP_NONE) ? 0 : op_units(g2, db.nt, db.mt);
   int slot, u, pr, pc;
   if (!map_slot(db, T1 + T2, slot, u)) return;
-  const GemmGeom g = u < T1 ? g1 : g2;  // block-uniform
-  if (u >= T1) {
-    u -= T1;
-    r0 = r02; c0 = c02; R = R2; C = C2; tri = tri2;
-  }
-  const int op = g.op;
-  int UR, UC;
-  unit_shape(op, UR, UC);
-  int np = 1, pr2 = 0, pc2 = 0;  // second (folded) unit
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  int wr = w / UC, wc = w - wr * UC;
-  if (tri) {  // lower-triangle tile 4u + w in row-major order (one call site of gemm_tile below:
-              // its cores are inlined once)
-    const int t = 4 * u + w;
-    if (t >= R * (R + 1) / 2) return;  // wave-uniform: the last unit's missing tiles
-    quad_tri(t, pr, pc);
-    wr = wc = 0;
+  // the wave's tiles: the plan's list, or the unit (and its folded mirror) of the decomposition
+  // below; ONE call site of gemm_tile (its cores are inlined once per kernel instance)
+  int np = 1, pr2 = 0, pc2 = 0, sel0 = 0, w8 = 0, wr = 0, wc = 0;
+  if (plan) {
+    w8 = 4 * u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    np = 4;
   } else {
-    const int RU = (R + UR - 1) / UR, CU = (C + UC - 1) / UC;
-    if (op == OP_SYRK) {
-      pr = UR * (u / CU);
-      pc = UC * (u % CU);
-    } else if (op == OP_TRSM) {  // K grows with the column: fold columns
-      const int nf = (CU + 1) / 2, pi = u / nf, f = u - pi * nf;
-      pr = pr2 = UR * pi;
-      pc = UC * (CU - 1 - f);
-      pc2 = UC * f;
-      np = (CU - 1 - f != f) ? 2 : 1;
-    } else {  // fold rows; TT: K shrinks with the row, LINV21 / PREDVAR: K grows with the row
-      const int f = u / CU, pj = u - f * CU;
-      const int lo = f, hi = RU - 1 - f;
-      pr = UR * (op == OP_TT ? lo : hi);
-      pr2 = UR * (op == OP_TT ? hi : lo);
-      pc = pc2 = UC * pj;
-      np = (lo != hi) ? 2 : 1;
+    if (u >= T1) {
+      u -= T1;
+      sel0 = 1;
+      r0 = r02; c0 = c02; R = R2; C = C2; tri = tri2;
+    }
+    const int op = (sel0 ? g2 : g1).op;  // block-uniform
+    int UR, UC;
+    unit_shape(op, UR, UC);
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    wr = w / UC;
+    wc = w - wr * UC;
+    if (tri) {  // lower-triangle tile 4u + w in row-major order
+      const int t = 4 * u + w;
+      if (t >= R * (R + 1) / 2) return;  // wave-uniform: the last unit's missing tiles
+      quad_tri(t, pr, pc);
+      wr = wc = 0;
+    } else {
+      const int RU = (R + UR - 1) / UR, CU = (C + UC - 1) / UC;
+      if (op == OP_SYRK) {
+        pr = UR * (u / CU);
+        pc = UC * (u % CU);
+      } else if (op == OP_TRSM) {  // K grows with the column: fold columns
+        const int nf = (CU + 1) / 2, pi = u / nf, f = u - pi * nf;
+        pr = pr2 = UR * pi;
+        pc = UC * (CU - 1 - f);
+        pc2 = UC * f;
+        np = (CU - 1 - f != f) ? 2 : 1;
+      } else {  // fold rows; TT: K shrinks with the row, LINV21 / PREDVAR: K grows with the row
+        const int f = u / CU, pj = u - f * CU;
+        const int lo = f, hi = RU - 1 - f;
+        pr = UR * (op == OP_TT ? lo : hi);
+        pr2 = UR * (op == OP_TT ? hi : lo);
+        pc = pc2 = UC * pj;
+        np = (lo != hi) ? 2 : 1;
+      }
     }
   }
 #pragma unroll 1
-  for (int pass = 0; pass < np; ++pass) {
-    const int ur = pass ? pr2 : pr, uc = pass ? pc2 : pc;
-    if (ur + wr >= R || uc + wc >= C) continue;  // wave-uniform: partial unit
+  for (int k = 0; k < np; ++k) {
+    int sel, ti, tj;
+    if (plan) {
+      const int e = N8_PLAN[w8][k];
+      if (e < 0) break;
+      sel = e >> 4;
+      ti = (sel ? r02 : r0) + ((e >> 2) & 3);
+      tj = (sel ? c02 : c0) + (e & 3);
+    } else {
+      const int ur = k ? pr2 : pr, uc = k ? pc2 : pc;
+      if (ur + wr >= R || uc + wc >= C) continue;  // wave-uniform: partial unit
+      sel = sel0;
+      ti = r0 + ur + wr;
+      tj = c0 + uc + wc;
+    }
     // wave-uniform tile indices in SGPRs (the 64 x 64 core needs every VGPR)
-    gemm_tile<PV, PM>(db, g, slot, __builtin_amdgcn_readfirstlane(r0 + ur + wr), __builtin_amdgcn_readfirstlane(c0 + uc + wc));
+    gemm_tile<PV, PM>(db, sel ? g2 : g1, slot, __builtin_amdgcn_readfirstlane(ti), __builtin_amdgcn_readfirstlane(tj));
   }
 }
 
@@ -2266,6 +2296,7 @@ void launch_gemm(const DevBatch& b, const GemmGeom& g, hipStream_t s, const Gemm
   }
   int T = op_units(g, b.nt, b.mt);
   if (g2.op != OP_NONE) T += op_units(g2, b.nt, b.mt);
+  if (n8_plan(g, g2)) T = 2;  // gemm_body's fixed plan
   const size_t lds = (g.op == OP_LINV21 || g2.op == OP_LINV21) ? 4 * 16 * TT_S * sizeof(double) : 0;
   if (g.op == OP_PREDVAR) hipLaunchKernelGGL(k_gemm_pv, dim3(grid_blocks(b.B, T)), dim3(NTHR), lds, s, b, g, g2);
   else if (g.op == OP_TRSM) hipLaunchKernelGGL(k_gemm<REV_B>, dim3(grid_blocks(b.B, T)), dim3(NTHR), lds, s, b, g, g2);
