@@ -656,6 +656,24 @@ __device__ __forceinline__ void leaf_ts(int o, int slot, int ev) {
 #else
 #define LEAF_TS(ev)
 #endif
+// ---- diagnostic build only (-DGPRX_GSTAMPS=op*100+n, scratch/gemm_timeline.py): per-wave
+// s_memrealtime of the GEMM launch of op at node size n: tile entry, core start, core end (loads
+// landed), epilogue end (stores landed), for the wave's first two tiles.  Not in the product build.
+#ifdef GPRX_GSTAMPS
+constexpr int GTS_MAX = 1 << 17;
+__device__ unsigned long long g_gts[GTS_MAX][8];
+__device__ __forceinline__ void gts(const GemmGeom& g, int pass, int ev) {
+  if (g.op * 100 + g.n != GPRX_GSTAMPS || pass > 1) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  const size_t i = (size_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if ((threadIdx.x & 63) == 0 && i < GTS_MAX) g_gts[i][4 * pass + ev] = t;
+}
+#define GTS(g, pass, ev) gts(g, pass, ev)
+#else
+#define GTS(g, pass, ev)
+#endif
 __device__ __forceinline__ void acc4_zero(d4 (&acc)[QM][QN]) {
 #pragma unroll
   for (int a = 0; a < QM; ++a)
@@ -1068,7 +1086,8 @@ __device__ __forceinline__ void diag_tile_fast(const DevBatch& db, int slot, int
 // One 64 x 64 output tile (ti, tj) of a GemmOp on one wave.
 constexpr int TT_S = TS + 2;  // row stride of k_gemm's per-wave transpose buffer (LINV21's Mt store)
 template <bool PV, int PM = PLAIN>
-__device__ __forceinline__ void gemm_tile(const DevBatch& db, const GemmGeom& g, int slot, int ti, int tj) {
+__device__ __forceinline__ void gemm_tile(const DevBatch& db, const GemmGeom& g, int slot, int ti, int tj, int pass = 0) {
+  GTS(g, pass, 0);
   const int op = PV ? (int)OP_PREDVAR : g.op;
   const size_t ld = db.ld, so = (size_t)slot * db.mat;
   int kb, ke;  // K range in tiles
@@ -1116,7 +1135,9 @@ __device__ __forceinline__ void gemm_tile(const DevBatch& db, const GemmGeom& g,
     // diagonal tile are skipped (mma_64x64_m); op and ti == tj are wave-uniform
     const int Kn = (ke - kb) * TS;
     const bool tri = (PM == TRI_A_FIRST && op == OP_TT) || (PM == REV_A && op == OP_LINV21) || (PM == REV_B && op == OP_TRSM);
+    GTS(g, pass, 1);
     mma_64x64_pm<PM>(acc, Ak, ld, Bk, ldb, Kn, tri);
+    GTS(g, pass, 2);
 #ifdef GPRX_STAMPS
     if ((op == OP_SYRK || op == OP_TT) && g.n == db.nt) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1159,6 +1180,7 @@ __device__ __forceinline__ void gemm_tile(const DevBatch& db, const GemmGeom& g,
         *p = (op == OP_SYRK ? -1.0 : sgn) * acc[a][b][q];  // SYRK: C - L L^T = -acc
       }
   if (op == OP_LINV21) zp_acc4(db, slot, ti, tj, acc, -1.0);
+  if (op != OP_LINV21) GTS(g, pass, 3);
   if (op == OP_LINV21) {  // Mt[tj, ti] = Linv[ti, tj]^T, transposed through LDS 16 rows at a time
     // so that every store instruction writes one contiguous 512-B column segment of Mt
     extern __shared__ __attribute__((aligned(16))) double gsm[];
@@ -1177,6 +1199,7 @@ __device__ __forceinline__ void gemm_tile(const DevBatch& db, const GemmGeom& g,
       for (int r = 0; r < 16; ++r) Mtt[(size_t)(16 * a + r) * ld + l] = tb[r * TT_S + l];
       __builtin_amdgcn_wave_barrier();
     }
+    GTS(g, pass, 3);
   }
 }
 
@@ -1261,7 +1284,7 @@ __device__ __forceinline__ void gemm_body(const DevBatch& db, const GemmGeom& g1
       tj = c0 + uc + wc;
     }
     // wave-uniform tile indices in SGPRs (the 64 x 64 core needs every VGPR)
-    gemm_tile<PV, PM>(db, sel ? g2 : g1, slot, __builtin_amdgcn_readfirstlane(ti), __builtin_amdgcn_readfirstlane(tj));
+    gemm_tile<PV, PM>(db, sel ? g2 : g1, slot, __builtin_amdgcn_readfirstlane(ti), __builtin_amdgcn_readfirstlane(tj), k);
   }
 }
 
@@ -2335,6 +2358,17 @@ void launch_rollout(const RolloutArgs& a, int dist_mode, hipStream_t s) {
 
 }  // namespace gprx
 
+#ifdef GPRX_GSTAMPS
+// diagnostic build only: copy (reset = 0) or clear (reset = 1) the GEMM tile timeline
+extern "C" int gprx_dbg_gts(unsigned long long* out, long long n, int reset) {
+  void* p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(gprx::g_gts)) != hipSuccess) return 3;
+  const size_t bytes = std::min<size_t>((size_t)n * 8, sizeof(gprx::g_gts));
+  if (hipDeviceSynchronize() != hipSuccess) return 3;
+  if (reset) return hipMemset(p, 0, sizeof(gprx::g_gts)) == hipSuccess ? 0 : 3;
+  return hipMemcpy(out, p, bytes, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 3;
+}
+#endif
 #ifdef GPRX_STAMPS
 // diagnostic build only: copy (reset = 0) or clear (reset = 1) stamp region `which`
 extern "C" int gprx_dbg_stamps(int which, unsigned long long* out, long long n, int reset) {
