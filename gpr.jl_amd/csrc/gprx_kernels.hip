@@ -671,8 +671,30 @@ __device__ __forceinline__ void gts(const GemmGeom& g, int pass, int ev) {
   if ((threadIdx.x & 63) == 0 && i < GTS_MAX) g_gts[i][4 * pass + ev] = t;
 }
 #define GTS(g, pass, ev) gts(g, pass, ev)
+// the gradient GEMM (GPRX_GSTAMPS=999): job entry, then per unit u: main loop start, main loop end,
+// unit end, at slots 1 + 3u ..; =998: unit 0 only, with its epilogue phases (gts_d)
+__device__ __forceinline__ void gts_d(int gu, int ev) {  // =998: unit 0's epilogue phases at slots 4..7
+  if (GPRX_GSTAMPS != 998 || gu != 0) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  const size_t i = (size_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if ((threadIdx.x & 63) == 0 && i < GTS_MAX) g_gts[i][ev] = t;
+}
+__device__ __forceinline__ void gts_l(int ev) {
+  if (GPRX_GSTAMPS != 999 && !(GPRX_GSTAMPS == 998 && ev < 4)) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  const size_t i = (size_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if ((threadIdx.x & 63) == 0 && i < GTS_MAX) g_gts[i][ev] = t;
+}
+#define GTS_L(ev) gts_l(ev)
+#define GTS_D(gu, ev) gts_d(gu, ev)
 #else
+#define GTS_D(gu, ev)
 #define GTS(g, pass, ev)
+#define GTS_L(ev)
 #endif
 __device__ __forceinline__ void acc4_zero(d4 (&acc)[QM][QN]) {
 #pragma unroll
@@ -1762,6 +1784,7 @@ __device__ __forceinline__ void lauum_body(const DevBatch& db) {
   int slot, job;
   if (!map_slot(db, db.nlj, slot, job)) return;
   const int* jb = db.lauum_order + (size_t)job * 2 * LU;
+  GTS_L(0);
   lauum_unit(db, slot, jb);
   if (jb[LU] >= 0) {  // block-uniform: the folded short unit
     __syncthreads();  // the first unit's LDS images and partials are consumed
@@ -1789,11 +1812,14 @@ __device__ __forceinline__ void lauum_unit(const DevBatch& db, int slot, const i
 #ifdef GPRX_STAMPS
   const Stamp st0 = stamp_now();
 #endif
+  [[maybe_unused]] const int gu = (ju - db.lauum_order) % (2 * LU) == 0 ? 0 : 1;  // the job's first or second unit
+  GTS_L(1 + 3 * gu);
   if (active) {  // wave-uniform: diagonal tiles form only their lower blocks
     const double* Ap = db.Mt + so + (size_t)ti * TS * ld + ti * TS;
     if (ti == tj) mma_64x64_m<TRI_AB_FIRST>(acc, Ap, ld, Ap, ld, (nt - ti) * TS);
     else mma_64x64_m<TRI_A_FIRST>(acc, Ap, ld, db.Mt + so + (size_t)ti * TS * ld + tj * TS, ld, (nt - ti) * TS);
   }
+  GTS_L(2 + 3 * gu);
 #ifdef GPRX_STAMPS
   if (active && (ju - db.lauum_order) % (2 * LU) == 0) {  // the job's first (long) unit
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1802,12 +1828,14 @@ __device__ __forceinline__ void lauum_unit(const DevBatch& db, int slot, const i
 #endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA landed
   __syncthreads();                                   // ... and every other wave's
+  GTS_D(gu, 4);
   double sf = 0.0, tr = 0.0;
   double* spw = sp + w * SPW;
   for (int e = l; e < SPW; e += 64) spw[e] = 0.0;
   const double* P = db.params + (size_t)slot * db.pst;
   for (int e = tid; e < nimg * TS; e += NTHR) als[e] = al[ju[2 + (e >> 6)] * TS + (e & 63)];
   __syncthreads();
+  GTS_D(gu, 5);
   if (active) {
     const double sf2 = P[d];
     const int ir = ju[15 + w], ic = ju[19 + w];
@@ -1847,6 +1875,7 @@ __device__ __forceinline__ void lauum_unit(const DevBatch& db, int slot, const i
         }
       }
     }
+    GTS_D(gu, 6);
     // row sums R (row 16a + lr over the tile's 64 columns), column sums C (column 16b + lk + 4q
     // over the 64 rows)
     double R[QM], Cs[QN][4];
@@ -1914,6 +1943,7 @@ __device__ __forceinline__ void lauum_unit(const DevBatch& db, int slot, const i
       __builtin_amdgcn_wave_barrier();
     }
   }
+  GTS_D(gu, 7);
   sf = wave_sum(sf);
   tr = wave_sum(tr);
   if (l == 0) {
@@ -1924,6 +1954,7 @@ __device__ __forceinline__ void lauum_unit(const DevBatch& db, int slot, const i
   double* out = db.grad_part + ((size_t)slot * db.ngu + ju[0]) * db.gps;
   for (int e = tid; e < d + 2; e += NTHR)
     out[e] = ((sp[e] + sp[SPW + e]) + sp[2 * SPW + e]) + sp[3 * SPW + e];
+  GTS_L(3 + 3 * gu);
 }
 __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_lauum_grad(DevBatch db) {
   lauum_body(db);

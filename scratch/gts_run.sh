@@ -8,3 +8,5 @@ for v in trsm32 trsm16 trsm8 syrk32 linv8; do
 done
 # builds (scratch/): for v in "trsm32 32" "trsm16 16" "trsm8 8" "syrk32 132" "linv8 308"; do set -- $v;
 #   bash varbuild.sh gts_$1 ../gpr.jl_amd/csrc/gprx_kernels.hip -DGPRX_GSTAMPS=$2; done
+#   bash varbuild.sh gts_lauum ../gpr.jl_amd/csrc/gprx_kernels.hip -DGPRX_GSTAMPS=999   (gemm_timeline.py --lauum)
+#   bash varbuild.sh gts_lau2 ../gpr.jl_amd/csrc/gprx_kernels.hip -DGPRX_GSTAMPS=998    (gemm_timeline.py --lau2)
