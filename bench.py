@@ -70,7 +70,7 @@ def make_workload(trials_per_gpu: int, rank: int, world: int):
 
 # library stat name -> kernel symbol (prefix) in rocprofv3 output; k_gemm serves several stats
 SYMBOL = {"gram": "k_gram", "leaf": "k_leaf", "diag": "k_diag", "alpha": "k_alpha", "lauum_grad": "k_lauum_grad",
-          "finalize": "k_finalize", "pred_cross": "k_pred_cross", "pred_final": "k_pred_final"}
+          "finalize": "k_finalize", "pred_cross": "k_pred_cross", "pred_final": "k_pred_final", "pred_var": "k_gemm_pv"}
 
 
 def pmc_traffic(stat: str, global_batch: int):

@@ -408,6 +408,35 @@ def test_production_path_b32_full_size(gprx, ctx):
     b.close()
 
 
+@pytest.mark.parametrize("N", [512, 1024, 960])
+def test_production_path_n8_plan(gprx, ctx, N):
+    """B >= 32 at N = 512 (the root is an 8-tile node: its SYRK + TT launch runs the fixed plan of
+    gemm_body, node tiles read from K), N = 1024 (two 8-tile children: the bottom one reads the
+    updated tiles from S) and N = 960 (15 tiles: 7/8-tile nodes, the plan only where h = 4);
+    slots against the oracle and bit-identical across runs."""
+    from gprx import data
+
+    B = 32
+    trs = [data.make_trial("P2", N, 100, seed=data.trial_seed("P2", 7 + t)) for t in range(B // 6 + 1)]
+    X = np.stack([trs[s // 6]["X"] for s in range(B)])
+    Y = np.stack([trs[s // 6]["Y"][s % 6] for s in range(B)])
+    Xs = np.stack([trs[s // 6]["Xs"] for s in range(B)])
+    rng = np.random.default_rng(N)
+    th0 = data.theta0("P2", 2048)
+    T = np.stack([th0 + 0.05 * rng.standard_normal(th0.shape[0]) for _ in range(B)])
+    b = gprx.GPBatch(B, 26, N, 100, ctx=ctx)
+    b.set_train(X, Y)
+    b.set_test(Xs)
+    r1 = b.run(T, grad=True, predict=True)
+    r2 = b.run(T, grad=True, predict=True)
+    assert np.all(r1["status"] == 0)
+    for k in ("mll", "grad", "mu", "var"):
+        np.testing.assert_array_equal(r1[k], r2[k])
+    for s in (0, 19, 31):
+        check_slot(r1, s, X[s], Y[s], T[s], Xs[s], ctx.dist_mode, strict=True)
+    b.close()
+
+
 def test_mean_only_prediction_matches_full(gprx, ctx, golden_dir):
     """var == NULL skips the variance GEMM; the means are bit-identical to the full prediction
     (GPE predict_y_mean: the predictdynamics.jl:13 rollout call)."""
