@@ -84,6 +84,11 @@ def local_trials(mech: str, N: int, variant: str, trial_ids, testsamples: int) -
                 d["mu"] = mdynamics.mean_min(mech, tr["X"], usesin)
                 d["Xs"] = data.min_features(mech, tr["start"], usesin)
         if md:
+            # a training column whose physics step fails (vi_step status 2, NaN) throws in the
+            # reference's GP construction: the trial is dropped; its GPs fit a finite dummy target
+            d["vi_failed"] = not np.all(np.isfinite(d["mu"]))
+            if d["vi_failed"]:
+                d["mu"] = np.nan_to_num(d["mu"], nan=0.0, posinf=0.0, neginf=0.0)
             d["Y_raw"] = d["Y"]
             d["Y"] = d["Y"] - d["mu"]  # the device fits y - μ(X) (mDynamics.jl: θ-independent mean)
         out.append(d)
@@ -110,6 +115,7 @@ def run_group(mech: str, N: int, variant: str, trial_ids, ctx, testsamples: int 
     t_opt = time.perf_counter() - t0
     G = rb.G
     ok_gp = opt["status"] == 0  # (n, G)
+    ok_gp &= np.array([[not t.get("vi_failed", False)] for t in trials])  # MeanDynamics mean failed: dropped
     err = np.full(n, math.inf)
     perr = np.zeros(n)
     # a trial whose experiment would throw in the reference (a failed refit: PosDefException /
@@ -142,7 +148,7 @@ def run_group(mech: str, N: int, variant: str, trial_ids, ctx, testsamples: int 
             starts = np.stack([trials[i]["Xs"].T for i in range(n)])  # (n, M, d)
             fin, pe, st = mdynamics.rollout_max(mech, rb, good, starts, simsteps, ctx=ctx)
             for k, i in enumerate(good):
-                if np.any(st[k] != 0):
+                if np.any(st[k] != 0) or np.isnan(fin[k]).any():  # singular projection / failed physics mean
                     continue
                 truth = data.test_truth(mech, testsamples, trials[i]["seed"], simsteps)["X"].T
                 err[i] = data.position_mse(truth, fin[k])
@@ -154,6 +160,8 @@ def run_group(mech: str, N: int, variant: str, trial_ids, ctx, testsamples: int 
             starts = np.stack([trials[i]["start"] for i in range(n)])  # (n, M, 2 nc)
             fin = mdynamics.rollout_min(mech, rb, good, starts, simsteps, usesin=variant == "md_min_sin")
             for k, i in enumerate(good):
+                if np.isnan(fin[k]).any():  # a failed physics mean (vi_step status 2) throws in the reference
+                    continue
                 truth = data.test_truth(mech, testsamples, trials[i]["seed"], simsteps)["X"].T
                 err[i] = data.position_mse(truth, fin[k])
                 failed[i] = False
@@ -189,13 +197,25 @@ def run_vi_baseline(mech: str, trial_ids, testsamples: int = 100, simsteps: int 
     (gprx.vi.simulate), error = simulationerror against the noise-free truth.  Host physics, no GP."""
     from . import vi
 
-    err = np.full(len(trial_ids), math.inf)
-    for k, t in enumerate(trial_ids):
-        seed = data.trial_seed(mech, t)
-        start = data.make_trial(mech, 2, testsamples, seed=seed)["Xs"].T
-        fin, _ = vi.simulate(mech, start, simsteps)
-        err[k] = data.position_mse(data.test_truth(mech, testsamples, seed, simsteps)["X"].T, fin)
-    return dict(kstep_mse=err)
+    n = len(trial_ids)
+    err = np.full(n, math.inf)
+    failed = np.zeros(n, dtype=bool)
+    if n == 0:
+        return dict(kstep_mse=err, failed=failed)
+    seeds = [data.trial_seed(mech, t) for t in trial_ids]
+    # every test start of every local trial in one vectorised simulation (the states are
+    # independent: each one's Newton iterates are those of a per-trial call)
+    start = np.concatenate([data.make_trial(mech, 2, testsamples, seed=sd)["Xs"].T for sd in seeds])
+    fin, st = vi.simulate(mech, start, simsteps)
+    for k, sd in enumerate(seeds):
+        sl = slice(k * testsamples, (k + 1) * testsamples)
+        # a test start whose physics step fails (vi_step status 2: the reference's DomainError /
+        # SingularException) throws the whole experiment: the trial is dropped (core.jl:41-53)
+        if np.any(st[sl] & 2):
+            failed[k] = True
+            continue
+        err[k] = data.position_mse(data.test_truth(mech, testsamples, sd, simsteps)["X"].T, fin[sl])
+    return dict(kstep_mse=err, failed=failed)
 
 
 def run(mechs=MECHS, sizes=SIZES, variants=VARIANTS, n_trials: int = 100, testsamples: int = 100, simsteps: int = 20,
@@ -217,13 +237,15 @@ def run(mechs=MECHS, sizes=SIZES, variants=VARIANTS, n_trials: int = 100, testsa
         if "vi" in variants:  # the pure variational-integrator baseline (noise.jl:72-75, idmod "VI")
             t0 = time.perf_counter()
             r = run_vi_baseline(mech, mine, testsamples, simsteps)
-            loc = {"kstep_mse": r["kstep_mse"].reshape(-1, 1), "t": np.full((len(mine), 1), time.perf_counter() - t0)}
+            loc = {"kstep_mse": r["kstep_mse"].reshape(-1, 1), "failed": r["failed"].astype(np.float64).reshape(-1, 1),
+                   "t": np.full((len(mine), 1), time.perf_counter() - t0)}
             g = shard.gather_results(loc, n_trials, lambda q: shard.shard_trials(n_trials, q, world), 0,
-                                     keys=("kstep_mse", "t")) if dist else loc
+                                     keys=("kstep_mse", "failed", "t")) if dist else loc
             if rank == 0:
+                keep = g["failed"][:, 0] == 0  # failed trials left out of the lists (core.jl:41-53)
                 results.setdefault("noisyVI", {})[f"{mech}_MIN2"] = {
-                    "nprocessed": n_trials, "kstep_mse": [float(v) for v in g["kstep_mse"][:, 0]],
-                    "projectionerror": [0.0] * n_trials, "variant": "vi"}
+                    "nprocessed": n_trials, "kstep_mse": [float(v) for v in g["kstep_mse"][keep, 0]],
+                    "projectionerror": [0.0] * int(keep.sum()), "variant": "vi", "dropped": int((~keep).sum())}
                 timing[f"{mech}_MIN2/vi"] = {"seconds_max_rank": float(np.max(g["t"][:, 0])) if n_trials else 0.0,
                                              "gp_fits": 0}
                 if log:

@@ -230,7 +230,8 @@ def _dphi_dw(q2, q3, w, dt=DT):
 def vi_step(mech_name: str, cstates, dt: float = DT, eps: float = 1e-10, newton_iter: int = 100):
     """newton!(mechanism) after setstates!(mechanism, CState(x)) for T states.  cstates (T, 13 nb)
     -> the solution CStates (T, 13 nb) = [x2, q2, v2, w2] per body (CState(mechanism,
-    usesolution=true), src/CState.jl:66-71), iterations (T,), status (T,) (1: not converged)."""
+    usesolution=true), src/CState.jl:66-71), iterations (T,), status (T,) (1: not converged; 2:
+    failed, where the reference throws (DomainError / SingularException): its row is NaN)."""
     mech = MECHANISMS[mech_name]
     nb = mech["nb"]
     cs = np.atleast_2d(np.asarray(cstates, dtype=np.float64))
@@ -252,6 +253,7 @@ def vi_step(mech_name: str, cstates, dt: float = DT, eps: float = 1e-10, newton_
     lam = np.zeros((T, nd))
     it = np.zeros(T, dtype=np.int32)
     done = np.zeros(T, dtype=bool)
+    failed = np.zeros(T, dtype=bool)
 
     def residual(a, v2a, w2a, lama):
         """residual of the states a (index array) at (v2a, w2a, lama)"""
@@ -284,7 +286,29 @@ def vi_step(mech_name: str, cstates, dt: float = DT, eps: float = 1e-10, newton_
             F[:, n6:, o + 3:o + 6] = Gphi3[:, :, o + 3:o + 6] @ _dphi_dw(q2[a, b], q3[:, b], w2[a, b], dt)
         if reg:
             F[:, n6:, n6:] -= reg * np.eye(nd)
-        ds = np.linalg.solve(F, f[..., None])[..., 0]
+        # a state whose system is not finite (|w| beyond 2/dt: the reference's sqrt throws a
+        # DomainError) or singular (LinearAlgebra's SingularException) fails alone: its solution
+        # is NaN and it leaves the iteration; the other states are solved as before
+        ds = np.full((na, n6 + nd), np.nan)
+        okf = np.nonzero(np.all(np.isfinite(F), axis=(1, 2)) & np.all(np.isfinite(f), axis=1))[0]
+        if len(okf):
+            try:
+                ds[okf] = np.linalg.solve(F[okf], f[okf][..., None])[..., 0]
+            except np.linalg.LinAlgError:
+                for j in okf:
+                    try:
+                        ds[j] = np.linalg.solve(F[j], f[j])
+                    except np.linalg.LinAlgError:
+                        pass
+        bad = ~np.all(np.isfinite(ds), axis=1)
+        if bad.any():
+            failed[a[bad]] = True
+            v2[a[bad]] = np.nan
+            w2[a[bad]] = np.nan
+            a, ds = a[~bad], ds[~bad]
+            na = len(a)
+            if na == 0:
+                break
         v2[a] -= ds[:, :n6].reshape(na, nb, 6)[..., 0:3]
         w2[a] -= ds[:, :n6].reshape(na, nb, 6)[..., 3:6]
         lam[a] -= ds[:, n6:]
@@ -296,7 +320,8 @@ def vi_step(mech_name: str, cstates, dt: float = DT, eps: float = 1e-10, newton_
         if len(a) == 0:
             break
     out = np.concatenate([x2, q2, v2, w2], axis=-1).reshape(T, 13 * nb)
-    return out, it, (~done).astype(np.int32)
+    out[failed] = np.nan
+    return out, it, np.where(failed, 2, (~done).astype(np.int32)).astype(np.int32)
 
 
 def mean_dynamics(mech_name: str, X, vw_indices, dt: float = DT):

@@ -124,3 +124,20 @@ def test_vi_baseline_simulates_steps_plus_one():
         ref, _, _ = vi.vi_step("P1", ref)
     np.testing.assert_array_equal(fin, ref)
     assert not bad.any()
+
+
+def test_failed_state_is_isolated():
+    """A state the reference cannot step (|w| beyond 2/dt: ConstrainedDynamics' sqrt throws a
+    DomainError) fails alone: status 2 and a NaN row; the other states' solutions are bit-identical
+    to a batch without it.  The sweep drops the trial of such a state (core.jl:41-53)."""
+    tr = data.make_trial("P2", 2, 3, seed=2)
+    S = tr["Xs"].T.copy()
+    good, _, st_good = vi.vi_step("P2", S)
+    bad = S.copy()
+    bad[1, 10:13] = 1e3 / vi.DT  # body 1's angular velocity far beyond 2/dt
+    out, _, st = vi.vi_step("P2", bad)
+    assert st[1] == 2 and np.isnan(out[1]).all()
+    np.testing.assert_array_equal(out[[0, 2]], good[[0, 2]])
+    np.testing.assert_array_equal(st[[0, 2]], st_good[[0, 2]])
+    fin, flags = vi.simulate("P2", bad, 2)
+    assert flags[1] & 2 and np.isnan(fin[1]).all() and np.isfinite(fin[[0, 2]]).all()
