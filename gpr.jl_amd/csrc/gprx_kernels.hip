@@ -1706,17 +1706,27 @@ __global__ __launch_bounds__(NTHR) void k_alpha(DevBatch db, int phase) {
   const int ng = (k1 - k0) / 16, g0 = (ng * w) / 4, g1 = (ng * (w + 1)) / 4;
   typedef double d2 __attribute__((ext_vector_type(2)));
   d2 acc[4] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};
+  // group gq + 1's loads are issued before group gq's arithmetic (16 loads in flight per lane)
+  d2 m[8];
+  if (g0 < g1) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) m[u] = *(const d2*)(A + (size_t)(k0 + 16 * g0 + 2 * u) * ld);
+  }
   for (int gq = g0; gq < g1; ++gq) {
     const int kk = k0 + 16 * gq;
-    d2 m[8];
+    d2 mn[8];
+    if (gq + 1 < g1) {
 #pragma unroll
-    for (int u = 0; u < 8; ++u) m[u] = *(const d2*)(A + (size_t)(kk + 2 * u) * ld);
+      for (int u = 0; u < 8; ++u) mn[u] = *(const d2*)(A + (size_t)(kk + 16 + 2 * u) * ld);
+    }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const double zv = cp ? v[kk + 2 * u + 1] : v[kk + 2 * u];
       acc[u & 3].x = fma(m[u].x, zv, acc[u & 3].x);
       acc[u & 3].y = fma(m[u].y, zv, acc[u & 3].y);
     }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) m[u] = mn[u];
   }
   double s0 = (acc[0].x + acc[1].x) + (acc[2].x + acc[3].x), s1 = (acc[0].y + acc[1].y) + (acc[2].y + acc[3].y);
   s0 += __shfl_xor(s0, 32);  // the other column parity
