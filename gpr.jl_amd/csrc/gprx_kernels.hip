@@ -932,11 +932,20 @@ __device__ __forceinline__ void diag_tile_fast(const DevBatch& db, int slot, int
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, lr = l & 15, lk = l >> 4;
   const size_t ld = db.ld;
   const double* A = Ksrc + (size_t)slot * db.mat + (size_t)jt * TS * ld + jt * TS;
-  for (int e = tid; e < TS * TS; e += NTHR) {
-    const int r = e & 63, c = e >> 6;
-    if (!t_ready) T[c * FS + r] = (r >= c) ? A[(size_t)c * ld + r] : 0.0;
-    Xi[c * FS + r] = 0.0;
+  if (!t_ready) {  // all 16 loads of a thread in flight before the LDS stores (one latency, not 16)
+    double v[TS * TS / NTHR];
+#pragma unroll
+    for (int k = 0; k < TS * TS / NTHR; ++k) {
+      const int e = tid + k * NTHR, r = e & 63, c = e >> 6;
+      v[k] = (r >= c) ? A[(size_t)c * ld + r] : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < TS * TS / NTHR; ++k) {
+      const int e = tid + k * NTHR, r = e & 63, c = e >> 6;
+      T[c * FS + r] = v[k];
+    }
   }
+  for (int e = tid; e < TS * TS; e += NTHR) Xi[(e >> 6) * FS + (e & 63)] = 0.0;
   __syncthreads();
   int fail = -1;
   double lsum = 0.0;  // wave 0: sum log l_jj
