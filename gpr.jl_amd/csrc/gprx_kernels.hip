@@ -1767,7 +1767,7 @@ __global__ __launch_bounds__(NTHR) void k_alpha(DevBatch db, int phase) {
 // 32 d distance evaluations and d wave reductions.  x is the centred copy Xc (per-dimension mean
 // removed; S_p is translation invariant), which keeps the expansion's cancellation at the
 // rounding level of the points' spread, as for the reference's own a^2 + b^2 - 2ab distances.
-// LDS: the unit's point tiles as raw [point][xs] images (LDS-DMA, issued before the MFMA loop),
+// LDS: the unit's point tiles as raw [point][xs] images (LDS-DMA, issued after the MFMA loop),
 // per-wave partials and alpha of the image points.
 // ============================================================================================
 __device__ __forceinline__ void dma_tile(double* lds, const double* src, int ndbl) {
@@ -1821,7 +1821,6 @@ __device__ __forceinline__ void lauum_unit(const DevBatch& db, int slot, const i
   const int nt = db.nt;
   const double* X = db.Xc + (size_t)slot * db.Npad * xs;
   const double* al = db.alpha + (size_t)slot * db.Npad;
-  for (int i = 0; i < nimg; ++i) dma_tile(img + i * xt, X + (size_t)ju[2 + i] * xt, xt);
   const int ti = ju[7 + w], tj = ju[11 + w];
   const bool active = ti >= 0;
   const int l = tid & 63, lr = l & 15, lk = l >> 4;
@@ -1845,6 +1844,9 @@ __device__ __forceinline__ void lauum_unit(const DevBatch& db, int slot, const i
     stamp_store(0, st0, stamp_now());
   }
 #endif
+  // the unit's point images by LDS-DMA after the main loop: issued before it, they sit ahead of
+  // the first stage's loads in the wave's in-order load counter and delay the first MFMA
+  for (int i = 0; i < nimg; ++i) dma_tile(img + i * xt, X + (size_t)ju[2 + i] * xt, xt);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA landed
   __syncthreads();                                   // ... and every other wave's
   GTS_D(gu, 4);
