@@ -921,14 +921,15 @@ constexpr int FS = TS + 1;  // LDS column stride of the tile images
 // t_ready: T already holds the tile's lower triangle (zeros above), written by the caller; else
 // it is read from Ksrc (K, or S when a SYRK updated it).
 __device__ __forceinline__ void diag_tile_fast(const DevBatch& db, int slot, int jt, double* T, double* Xi, double* cbs,
-                                               bool t_ready, const double* Ksrc);
+                                               bool t_ready, const double* Ksrc, bool store = true);
+__device__ __forceinline__ void diag_store(const DevBatch& db, int slot, int jt, const double* Xi, double* cbs);
 __global__ __launch_bounds__(NTHR) void k_diag_f(DevBatch db, int jt, int upd) {
   __shared__ double T[TS * FS], Xi[TS * FS];
   __shared__ __attribute__((aligned(16))) double cbs[256];
   if (slot_active(db, blockIdx.x)) diag_tile_fast(db, blockIdx.x, jt, T, Xi, cbs, false, upd ? db.S : db.K);
 }
 __device__ __forceinline__ void diag_tile_fast(const DevBatch& db, int slot, int jt, double* T, double* Xi, double* cbs,
-                                               bool t_ready, const double* Ksrc) {
+                                               bool t_ready, const double* Ksrc, bool store) {
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, lr = l & 15, lk = l >> 4;
   const size_t ld = db.ld;
   const double* A = Ksrc + (size_t)slot * db.mat + (size_t)jt * TS * ld + jt * TS;
@@ -1096,6 +1097,14 @@ __device__ __forceinline__ void diag_tile_fast(const DevBatch& db, int slot, int
       }
     }
   }
+  if (store) diag_store(db, slot, jt, Xi, cbs);
+}
+// The diagonal routine's results to HBM: Linv[jt,jt], Mt[jt,jt] and the tile's z partial, from the
+// inverse image Xi (LDS).  The fused leaf issues them after its TRSM tasks' loads: issued first, the
+// stores sat ahead of those loads in the in-order counter and zp_diag's barriers drained them.
+__device__ __forceinline__ void diag_store(const DevBatch& db, int slot, int jt, const double* Xi, double* cbs) {
+  const int tid = threadIdx.x;
+  const size_t ld = db.ld;
   double* Li = db.Linv + (size_t)slot * db.mat + (size_t)jt * TS * ld + jt * TS;
   double* Mj = db.Mt + (size_t)slot * db.mat + (size_t)jt * TS * ld + jt * TS;
   for (int e = tid; e < TS * TS; e += NTHR) {
@@ -1552,7 +1561,7 @@ __device__ __forceinline__ void leaf_body(const DevBatch& db, int o, int n, int 
     const int tk = o + k, m = n - 1 - k;
     const double* xi = dXi;  // Linv[tk,tk] in LDS, read by the TRSM tasks below
     const double* K = k > 0 ? S : K0;
-    diag_tile_fast(db, slot, tk, dT, dXi, dcb, k > 0, upd ? db.S : db.K);  // k > 0: the SYRK below left the tile in dT
+    diag_tile_fast(db, slot, tk, dT, dXi, dcb, k > 0, upd ? db.S : db.K, false);  // k > 0: the SYRK below left the tile in dT
     __syncthreads();
     LEAF_TS(1 + 3 * k);
     for (int t = 0; t < m; ++t) {  // TRSM: L[ti,tk] = K[ti,tk] Linv[tk,tk]^T
@@ -1563,6 +1572,7 @@ __device__ __forceinline__ void leaf_body(const DevBatch& db, int o, int n, int 
       mma_64x16(acc, K + (size_t)tk * TS * ld + ti * TS, ld, xi + cq, FS, TS);
       accq_store(Lw + (size_t)(tk * TS + cq) * ld + ti * TS, ld, acc, 1.0);
     }
+    diag_store(db, slot, tk, dXi, dcb);  // after the TRSM loads (dXi stays until the next diagonal)
     __syncthreads();
     LEAF_TS(2 + 3 * k);
     for (int c = 0; c < m; ++c)  // SYRK (lower trailing tiles)
