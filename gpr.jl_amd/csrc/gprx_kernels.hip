@@ -1766,8 +1766,9 @@ __global__ __launch_bounds__(NTHR) void k_alpha(DevBatch db, int phase) {
 //   G_rc = wt_rc * (alpha_r alpha_c - Kinv_rc) * Kf_rc    (wt = 1/2 on the diagonal, as
 //                                                        dmll_kern! weights ααinvcKI[j,j]/2)
 //   S_p = sum G_rc (x_pr - x_pc)^2,  S_f = sum G_rc,  T = sum_diag W_rr
-// One gradient partial row per unit of 4 tiles.  Kf is the Gram's own noise-free copy (upper
-// tiles of K, diagonal tiles in Kd), read once per output tile.
+// One gradient partial row per unit of 4 tiles.  Kf is K's lower tile (ti, tj) exactly as the Gram
+// wrote it (the factorisation's SYRKs write S, never K), read once per output tile; only entries
+// with gi > gj are used, so the noise on the diagonal is never seen: G_rr uses sf2 analytically.
 //
 // The distance sums are expanded per wave tile (rows r, columns c):
 //   S_p = sum_r x_pr^2 R_r + sum_c x_pc^2 C_c - 2 sum_r x_pr Q_rp,   Q = G Xc  (64 x d)
@@ -1874,8 +1875,9 @@ __device__ __forceinline__ void lauum_unit(const DevBatch& db, int slot, const i
     const double* xc = img + ic * xt;  // [c][xs]
     const double* ar = als + ir * TS;
     const double* ac = als + ic * TS;
-    // G in place of acc, with Kf read back from the Gram's noise-free copy (upper tile (tj, ti) of K,
-    // or Kd for a diagonal tile): the same kernel values the factorisation used
+    // G in place of acc, with Kf read from K's lower tile (ti, tj) as the Gram wrote it (the same
+    // kernel values the factorisation used); only gi > gj is used: the diagonal (Kf + noise) is
+    // never loaded, G_rr = W_rr sf2 / 2 analytically
     const double* Kf = db.K + so + (size_t)(tj * TS) * ld + ti * TS;
     const size_t ldk = ld;
 #pragma unroll

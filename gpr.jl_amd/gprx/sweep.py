@@ -53,6 +53,16 @@ VARIANTS = ("vi", "max", "min", "min_sin", "md_max", "md_min", "md_min_sin")  # 
 # parallelsim idmod (noise.jl:80-85): etype = "noisy" * idmod
 ETYPE = {"max": "noisy", "min": "noisy", "min_sin": "noisysin", "md_max": "noisyMD", "md_min": "noisyMD",
          "md_min_sin": "noisyMDsin"}
+# What each entry's numbers are checked against.  The vi baseline and the md_* variants depend on a
+# host restatement of ConstrainedDynamics 0.7.4's variational-integrator step (gprx.vi), which is not
+# in the reference tree: its only cross-check is the repo's own action-based oracle/vi_oracle.py
+# (same modelling assumptions), so those entries are not reference-equivalent numbers.
+PARITY = {"max": "gp: oracle-pinned; physics: projectv! restated (unpinned vs ConstrainedDynamics)",
+          "min": "gp: oracle-pinned", "min_sin": "gp: oracle-pinned",
+          "vi": "unpinned: gprx.vi restates ConstrainedDynamics 0.7.4 newton! (absent from the reference tree)",
+          "md_max": "unpinned: MeanDynamics mean from gprx.vi (ConstrainedDynamics absent)",
+          "md_min": "unpinned: MeanDynamics mean from gprx.vi (ConstrainedDynamics absent)",
+          "md_min_sin": "unpinned: MeanDynamics mean from gprx.vi (ConstrainedDynamics absent)"}
 
 
 def _dist():
@@ -245,7 +255,8 @@ def run(mechs=MECHS, sizes=SIZES, variants=VARIANTS, n_trials: int = 100, testsa
                 keep = g["failed"][:, 0] == 0  # failed trials left out of the lists (core.jl:41-53)
                 results.setdefault("noisyVI", {})[f"{mech}_MIN2"] = {
                     "nprocessed": n_trials, "kstep_mse": [float(v) for v in g["kstep_mse"][keep, 0]],
-                    "projectionerror": [0.0] * int(keep.sum()), "variant": "vi", "dropped": int((~keep).sum())}
+                    "projectionerror": [0.0] * int(keep.sum()), "variant": "vi", "dropped": int((~keep).sum()),
+                    "parity": PARITY["vi"]}
                 timing[f"{mech}_MIN2/vi"] = {"seconds_max_rank": float(np.max(g["t"][:, 0])) if n_trials else 0.0,
                                              "gp_fits": 0}
                 if log:
@@ -276,7 +287,7 @@ def run(mechs=MECHS, sizes=SIZES, variants=VARIANTS, n_trials: int = 100, testsa
                                                        "kstep_mse": [float(v) for v in g["kstep_mse"][keep, 0]],
                                                        "projectionerror": [float(v) for v in g["perr"][keep, 0]],
                                                        "variant": var, "ok": int(g["ok"][:, 0].sum()),
-                                                       "dropped": int((~keep).sum())}
+                                                       "dropped": int((~keep).sum()), "parity": PARITY[var]}
                     timing[f"{key}/{var}"] = {"seconds_max_rank": float(np.max(g["t"][:, 0])) if n_trials else 0.0,
                                               "gp_fits": n_trials * (len(data.VW_INDICES[mech]) if var.endswith("max")
                                                                      else NCOORD[mech])}
@@ -297,7 +308,7 @@ def main(argv=None):
     ap.add_argument("--trials", type=int, default=100)
     ap.add_argument("--testsamples", type=int, default=100)
     ap.add_argument("--simsteps", type=int, default=20)
-    ap.add_argument("--max-evals", type=int, default=30, help="evaluation budget per GP (<0: none)")
+    ap.add_argument("--max-evals", type=int, default=30, help="evaluation budget per GP (<= 0: none, as Optim's f_calls_limit)")
     ap.add_argument("--time-limit", type=float, default=float("nan"), help="seconds per group call (NaN: none)")
     ap.add_argument("--out", default="gpurun_out/sweep_final_checkpoint.json")
     ap.add_argument("--rehearse", action="store_true", help="allow ranks to share GPUs (gloo control plane)")
@@ -306,7 +317,7 @@ def main(argv=None):
     t0 = time.perf_counter()
     res = run([m for m in a.mechs.split(",") if m], [int(s) for s in a.sizes.split(",") if s],
               [v for v in a.variants.split(",") if v], a.trials, a.testsamples, a.simsteps,
-              None if a.max_evals < 0 else a.max_evals, a.time_limit,
+              a.max_evals if a.max_evals > 0 else None, a.time_limit,
               log=lambda s: print(s, flush=True))
     wall = time.perf_counter() - t0
     if res is not None:

@@ -40,7 +40,11 @@
 extern "C" {
 #endif
 
-#define GPRX_ABI_VERSION 1
+/* ABI versions:
+ *   1  first release.
+ *   2  gprx_opt_options.max_evals <= 0 means "no limit" (Optim's f_calls_limit = 0); under
+ *      version 1, 0 was a real cap of zero evaluations.  No signature changed. */
+#define GPRX_ABI_VERSION 2
 
 /* status codes (mirrors the reference's failure modes) */
 #define GPRX_OK 0

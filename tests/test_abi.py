@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version_and_status_strings():
-    assert L.lib.gprx_abi_version() == 1
+    assert L.lib.gprx_abi_version() == 2
     assert L.lib.gprx_status_string(1) == b"not positive definite"
 
 
