@@ -1008,6 +1008,21 @@ static bool build_mech(int mech, gprx::MechDev& M) {
       break;
     default: return false;
   }
+  // bodies as examples/utils/data/simulations.jl builds them (gprx/vi.py MECHANISMS): m = 1, J = I m
+  // l^2 / 12 for the unit links, the cart-pole's pole l = 0.5 (I / 48) and its cart a 0.2 x 0.3 x 0.1
+  // box, diag(y^2 + z^2, x^2 + z^2, x^2 + y^2) m / 12
+  for (int b = 0; b < M.nb; ++b) {
+    M.m[b] = 1.0;
+    for (int r = 0; r < 3; ++r)
+      for (int c = 0; c < 3; ++c) M.J[b][r][c] = r == c ? 1.0 / 12.0 : 0.0;
+  }
+  if (mech == GPRX_MECH_CP) {
+    const double x = 0.2, y = 0.3, z = 0.1;
+    M.J[0][0][0] = (y * y + z * z) * 1.0 / 12.0;
+    M.J[0][1][1] = (x * x + z * z) * 1.0 / 12.0;
+    M.J[0][2][2] = (x * x + y * y) * 1.0 / 12.0;
+    for (int r = 0; r < 3; ++r) M.J[1][r][r] = 1.0 / 48.0;
+  }
   int row = 0;
   M.nsub = (int)js.size();
   for (int k = 0; k < M.nsub; ++k) {
@@ -1093,6 +1108,48 @@ int gprx_projectv(gprx_ctx* c, int mech, double dt, int T, const double* cstates
   timed(c, c->stream, "projectv", 0.0, (double)T * 8.0 * (13 + 12) * nb, [&] { gprx::launch_project(a, c->stream); });
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipMemcpyAsync(vw_out, base + o_out, (size_t)T * 6 * nb * 8, hipMemcpyDeviceToHost, c->stream));
+  std::vector<int> it(T), st(T);
+  HIPCHK(c, hipMemcpyAsync(it.data(), base + o_it, (size_t)T * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(st.data(), base + o_st, (size_t)T * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  collect(c);
+  if (iterations) memcpy(iterations, it.data(), (size_t)T * 4);
+  if (status) memcpy(status, st.data(), (size_t)T * 4);
+  return GPRX_OK;
+}
+
+int gprx_vi_step(gprx_ctx* c, int mech, double dt, int T, const double* cstates, double regularizer, int newton_iter,
+                 double eps, double* out, int* iterations, int* status) {
+  if (!c) return GPRX_INVALID_ARGUMENT;
+  gprx::MechDev M;
+  if (!build_mech(mech, M) || T < 0 || newton_iter < 0 || !(dt > 0.0) || !std::isfinite(regularizer) || !(eps >= 0.0))
+    return set_err(c, GPRX_INVALID_ARGUMENT, "gprx_vi_step: bad mechanism / T / newton_iter / dt / regularizer / eps");
+  if (T == 0) return GPRX_OK;
+  if (!cstates || !out) return set_err(c, GPRX_INVALID_ARGUMENT, "gprx_vi_step: null argument");
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess) return GPRX_DEVICE_ERROR;
+  const int nb = M.nb;
+  const size_t o_cs = 0, o_out = al16(o_cs + (size_t)T * 13 * nb * 8), o_it = al16(o_out + (size_t)T * 13 * nb * 8),
+               o_st = al16(o_it + (size_t)T * 4), need = al16(o_st + (size_t)T * 4);
+  char* base;
+  int rc = ctx_scratch(c, need, &base);
+  if (rc) return rc;
+  HIPCHK(c, hipMemcpyAsync(base + o_cs, cstates, (size_t)T * 13 * nb * 8, hipMemcpyHostToDevice, c->stream));
+  gprx::ViArgs a{};
+  a.mech = M;
+  a.dt = dt;
+  a.reg = regularizer;
+  a.eps = eps;
+  a.grav = 9.81;  // |mechanism.g| (simulations.jl; gprx/vi.py GRAV)
+  a.iters = newton_iter;
+  a.T = T;
+  a.cs = (const double*)(base + o_cs);
+  a.out = (double*)(base + o_out);
+  a.iters_out = (int*)(base + o_it);
+  a.status = (int*)(base + o_st);
+  timed(c, c->stream, "vi_step", 0.0, (double)T * 8.0 * 26 * nb, [&] { gprx::launch_vi_step(a, c->stream); });
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(out, base + o_out, (size_t)T * 13 * nb * 8, hipMemcpyDeviceToHost, c->stream));
   std::vector<int> it(T), st(T);
   HIPCHK(c, hipMemcpyAsync(it.data(), base + o_it, (size_t)T * 4, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipMemcpyAsync(st.data(), base + o_st, (size_t)T * 4, hipMemcpyDeviceToHost, c->stream));

@@ -135,6 +135,8 @@ struct SubJoint {
 struct MechDev {
   int nb, nd, nsub;  // bodies, constraint rows, sub-joints
   SubJoint sub[PJ_MAXSUB];
+  double m[PJ_MAXB];        // body masses and inertia tensors (body frame; the variational
+  double J[PJ_MAXB][3][3];  // integrator's dynamics, k_vi_step)
 };
 struct ProjArgs {
   MechDev mech;
@@ -159,7 +161,20 @@ struct RolloutMaxArgs {
   double* perr;         // T mean projection error per step
   int* status;          // T
 };
+// One variational-integrator step (ConstrainedDynamics 0.7.4 newton!, restated in gprx/vi.py) for T
+// independent states: the MeanDynamics prior mean (src/mDynamics.jl:41-60).
+struct ViArgs {
+  MechDev mech;
+  double dt, reg, eps, grav;
+  int iters;          // newtonIter
+  int T;
+  const double* cs;   // T x 13 nb current CStates
+  double* out;        // T x 13 nb solution CStates [x2, q2, v2, w2] per body (NaN row: failed)
+  int* iters_out;     // T Newton iterations
+  int* status;        // T: 0 converged, 1 not converged, 2 failed (non-finite / singular system)
+};
 void launch_project(const ProjArgs& a, hipStream_t s);
+void launch_vi_step(const ViArgs& a, hipStream_t s);
 void launch_rollout_max(const RolloutMaxArgs& a, int dist_mode, hipStream_t s);
 
 // hyper-parameters -> kernel parameters for one slot, exactly as SEArd / GPE derive them:

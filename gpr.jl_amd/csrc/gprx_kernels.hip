@@ -189,6 +189,29 @@ __device__ __forceinline__ double row_sum16(double v) {
   return v;
 }
 
+// lane m of each row of 16 lanes, broadcast to the row (DPP row_newbcast, gfx90a+; m folds to a
+// constant once the caller's loop is unrolled)
+__device__ __forceinline__ double row_bcast16(double v, int m) {
+  switch (m & 15) {
+    case 0: return dpp_f64<0x150>(v);
+    case 1: return dpp_f64<0x151>(v);
+    case 2: return dpp_f64<0x152>(v);
+    case 3: return dpp_f64<0x153>(v);
+    case 4: return dpp_f64<0x154>(v);
+    case 5: return dpp_f64<0x155>(v);
+    case 6: return dpp_f64<0x156>(v);
+    case 7: return dpp_f64<0x157>(v);
+    case 8: return dpp_f64<0x158>(v);
+    case 9: return dpp_f64<0x159>(v);
+    case 10: return dpp_f64<0x15A>(v);
+    case 11: return dpp_f64<0x15B>(v);
+    case 12: return dpp_f64<0x15C>(v);
+    case 13: return dpp_f64<0x15D>(v);
+    case 14: return dpp_f64<0x15E>(v);
+    default: return dpp_f64<0x15F>(v);
+  }
+}
+
 // per-tile partials of z = L^-1 y (see zp_acc4)
 __device__ __forceinline__ double* zp_row(const DevBatch& db, int slot, int h) {
   return db.zp + ((size_t)slot * 2 * db.nt + h) * db.Npad;
@@ -953,12 +976,20 @@ __device__ __forceinline__ void diag_tile_fast(const DevBatch& db, int slot, int
   for (int P = 0; P < 4; ++P) {
     const int c0 = 16 * P;
     if (w == 0) {
-      // ---- factor the diagonal block: lane i < 16 holds row i (a[k] = A[c0+i][c0+k]); the
-      //      scaled column j is published in LDS (cb) and read back as broadcasts ----
-      double* cb = cbs;  // scratch: column j of L during the factor, then the row-major L block
-      double a[16], ri[16];
+      // ---- factor and invert the diagonal block together, by elimination on 16 lanes: lane i
+      //      holds row i of the block (a[k] = A[c0+i][c0+k], becoming L) and column i of its
+      //      inverse (y[m] = X[m][i], starting from the identity).  Step j scales column j of L and
+      //      row j of X by 1/l_jj, then L[m][j] (lane m's a[j]) is broadcast to the row of 16 lanes
+      //      by DPP (row_newbcast: no LDS round trip) and updates both A (a[m] -= L[i][j] L[m][j])
+      //      and X (X[m][i] -= L[m][j] X[j][i]).  The operations and their order are those of the
+      //      column-by-column factor followed by the row-oriented forward substitution, so the
+      //      results are bit-identical to that form. ----
+      double a[16], y[16];
 #pragma unroll
-      for (int k = 0; k < 16; ++k) a[k] = T[(c0 + k) * FS + c0 + lr];
+      for (int k = 0; k < 16; ++k) {
+        a[k] = T[(c0 + k) * FS + c0 + lr];
+        y[k] = (k == lr) ? 1.0 : 0.0;
+      }
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
         const double p = readlane_d(a[j], j);
@@ -966,46 +997,16 @@ __device__ __forceinline__ void diag_tile_fast(const DevBatch& db, int slot, int
         if (!(p > 0.0) && fail < 0) fail = c0 + j;
         double ljj, rj;
         sqrt_rsqrt(pk, ljj, rj);
-        ri[j] = rj;
         a[j] = (lr > j) ? a[j] * rj : (lr == j ? ljj : 0.0);
-        if (j < 15) {
-          if (l < 16) cb[j * 16 + l] = a[j];  // column j of L (row-major scratch: cb[j*16 + i])
-          __builtin_amdgcn_wave_barrier();
-          double lk[16];
+        y[j] = y[j] * rj;
 #pragma unroll
-          for (int k = (j + 1) & ~1; k < 16; k += 2) {
-            const double2 v = *(const double2*)(cb + j * 16 + k);
-            lk[k] = v.x;
-            lk[k + 1] = v.y;
-          }
-#pragma unroll
-          for (int k = j + 1; k < 16; ++k) a[k] = fma(-a[j], lk[k], a[k]);
+        for (int m = j + 1; m < 16; ++m) {
+          const double b = row_bcast16(a[j], m);  // L[m][j]
+          a[m] = fma(-a[j], b, a[m]);
+          y[m] = fma(-b, y[j], y[m]);
         }
       }
-      // L block row-major into the scratch (cb[i*16 + k] = L[i][k]) for the inverse's broadcasts
-      __builtin_amdgcn_wave_barrier();
-      if (l < 16) {
-#pragma unroll
-        for (int k = 0; k < 16; k += 2) *(double2*)(cb + l * 16 + k) = make_double2(a[k], a[k + 1]);
-      }
-      __builtin_amdgcn_wave_barrier();
-      // ---- inverse of the block: lane c < 16 holds column c of X (x[r] = X[r][c]) ----
-      double x[16];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        double Lr[16];
-#pragma unroll
-        for (int m = 0; m < (r & ~1); m += 2) {
-          const double2 v = *(const double2*)(cb + r * 16 + m);
-          Lr[m] = v.x;
-          Lr[m + 1] = v.y;
-        }
-        if (r & 1) Lr[r - 1] = cb[r * 16 + r - 1];
-        double t = (r == lr) ? 1.0 : 0.0;
-#pragma unroll
-        for (int m = 0; m < r; ++m) t = fma(-Lr[m], x[m], t);
-        x[r] = t * ri[r];
-      }
+      double (&x)[16] = y;
       if (l < 16) {
 #pragma unroll
         for (int k = 0; k < 16; ++k) T[(c0 + k) * FS + c0 + l] = (k <= l) ? a[k] : 0.0;  // row l of L_PP
@@ -1810,15 +1811,23 @@ __host__ __device__ inline size_t lauum_lds_dbl(int xs, int nimg) {
 // would cost a workgroup per CU against 4 (d > 26 at two per CU, d > 63 at one), the plan falls
 // back to 2 x 2 units.
 __device__ __forceinline__ void lauum_unit(const DevBatch& db, int slot, const int* ju);
+#ifndef GPRX_LAUUM_STAGGER
+#define GPRX_LAUUM_STAGGER 0
+#endif
 __device__ __forceinline__ void lauum_body(const DevBatch& db) {
   int slot, job;
   if (!map_slot(db, db.nlj, slot, job)) return;
   const int* jb = db.lauum_order + (size_t)job * 2 * LU;
   GTS_L(0);
-  lauum_unit(db, slot, jb);
-  if (jb[LU] >= 0) {  // block-uniform: the folded short unit
+  const int nu = jb[LU] >= 0 ? 2 : 1;  // block-uniform: the folded short unit
+  // stagger: half of the workgroups take their short unit first, so that the two workgroups on a
+  // CU (one wave each per SIMD) reach their epilogues at different times
+  const int sw = nu == 2 && (GPRX_LAUUM_STAGGER == 1 ? ((blockIdx.x >> 8) & 1)
+                                                      : GPRX_LAUUM_STAGGER == 2 ? (__popc(blockIdx.x * 0x9E3779B1u) & 1) : 0);
+  lauum_unit(db, slot, jb + (sw ? LU : 0));
+  if (nu == 2) {
     __syncthreads();  // the first unit's LDS images and partials are consumed
-    lauum_unit(db, slot, jb + LU);
+    lauum_unit(db, slot, jb + (sw ? 0 : LU));
   }
 }
 __device__ __forceinline__ void lauum_unit(const DevBatch& db, int slot, const int* ju) {

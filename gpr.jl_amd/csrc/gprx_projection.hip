@@ -130,7 +130,8 @@ __device__ __forceinline__ void pose3(const PState& P, int b, double dt, double*
 
 // One sub-joint's constraint rows (into f[n6 + row0 ..] when want_g) and, when want_jac, its
 // Jacobian blocks into F (G rows and the transposed G^T columns).  Called by one lane.
-__device__ void subjoint(PState& P, const SubJoint& J, int n6, int ldf, double dt, bool want_g, bool want_jac) {
+__device__ void subjoint(PState& P, const SubJoint& J, int n6, int ldf, double dt, bool want_g, bool want_jac,
+                         bool sym = true) {
   double xa[3], xb[3];
   Qd qa, qb;
   pose3(P, J.a, dt, xa, qa);
@@ -236,8 +237,10 @@ __device__ void subjoint(PState& P, const SubJoint& J, int n6, int ldf, double d
           }
           PJ_F[row * ldf + c0 + j] = tv;
           PJ_F[row * ldf + c0 + 3 + j] = tw;
-          PJ_F[(c0 + j) * ldf + row] = tv;
-          PJ_F[(c0 + 3 + j) * ldf + row] = tw;
+          if (sym) {
+            PJ_F[(c0 + j) * ldf + row] = tv;
+            PJ_F[(c0 + 3 + j) * ldf + row] = tw;
+          }
         }
       }
     }
@@ -272,6 +275,83 @@ __device__ __forceinline__ void pj_sync() {
   } else {
     __syncthreads();
   }
+}
+
+// A x = b by LAPACK dgetf2's right-looking LU with partial pivoting (first maximal |pivot|,
+// reciprocal scaling, rank-1 update spread over the NW waves, one element per thread) and dgetrs'
+// unit-lower / upper substitutions, as Julia's F \ f.  A (n x n, row stride ldf) in LDS is
+// overwritten; b: lane l < n holds b_l on entry and x_l on exit (the same on every wave).  Returns
+// true for an exactly singular pivot (b is then undefined).  All NW * 64 threads call.
+template <int NW>
+__device__ bool lu_solve(double* A, int n, int ldf, double& b) {
+  constexpr int NT = 64 * NW;
+  const int tid = threadIdx.x & (NT - 1), l = tid & 63;
+  const bool w0 = tid < 64;
+  bool singular = false;
+  for (int k = 0; k < n; ++k) {
+    // pivot: first row of maximal |a_ik|, i >= k (idamax)
+    double v = (l >= k && l < n) ? fabs(A[l * ldf + k]) : -1.0;
+    int idx = l;
+    for (int o = 1; o < 64; o <<= 1) {
+      const double v2 = __shfl_xor(v, o);
+      const int i2 = __shfl_xor(idx, o);
+      if (v2 > v || (v2 == v && i2 < idx)) {
+        v = v2;
+        idx = i2;
+      }
+    }
+    const int p = idx;
+    if (p != k) {  // swap rows k and p of A and of the right-hand side
+      if (NW > 1) pj_sync<NW>();  // every wave has read column k
+      for (int j = tid; j < n; j += NT) {
+        const double t = A[k * ldf + j];
+        A[k * ldf + j] = A[p * ldf + j];
+        A[p * ldf + j] = t;
+      }
+      const double bk = readlane_dbl(b, k), bp = readlane_dbl(b, p);
+      if (l == k) b = bp;
+      if (l == p) b = bk;
+    }
+    pj_sync<NW>();
+    const double akk = A[k * ldf + k];
+    if (akk == 0.0) singular = true;
+    const int m = n - 1 - k;
+    if (akk != 0.0 && m > 0) {
+      if (w0 && l > k && l < n)
+        A[l * ldf + k] = fabs(akk) >= DBL_MIN ? A[l * ldf + k] * (1.0 / akk) : A[l * ldf + k] / akk;
+      pj_sync<NW>();
+      // trailing update A[i][j] -= l_i A[k][j], i, j in (k, n): element e = (i - k - 1) m + (j - k - 1)
+      const int si = NT / m, sj = NT - si * m;
+      int i = tid / m, j = tid - i * m;
+      for (int e = tid; e < m * m; e += NT) {
+        const int gi = k + 1 + i, gj = k + 1 + j;
+        A[gi * ldf + gj] = A[gi * ldf + gj] - A[gi * ldf + k] * A[k * ldf + gj];
+        i += si;
+        j += sj;
+        if (j >= m) {
+          j -= m;
+          ++i;
+        }
+      }
+    }
+    pj_sync<NW>();
+  }
+  if (singular) return true;
+  // forward substitution (unit lower), then backward (upper), as dgetrs / dtrsm
+  for (int k = 0; k < n; ++k) {
+    const double bk = readlane_dbl(b, k);
+    if (bk != 0.0 && l > k && l < n) b = b - bk * A[l * ldf + k];
+  }
+  for (int k = n - 1; k >= 0; --k) {
+    const double ukk = A[k * ldf + k];
+    double bk = readlane_dbl(b, k);
+    if (bk != 0.0) {
+      bk = bk / ukk;
+      if (l == k) b = bk;
+      if (l < k) b = b - bk * A[l * ldf + k];
+    }
+  }
+  return false;
 }
 
 // projectv! on NW waves (all NW * 64 threads call).  P.s holds the predicted (v, w) per body on
@@ -311,73 +391,10 @@ __device__ void project(PState& P, const MechDev& M, double dt, double reg, doub
     for (int i = tid; i < n * ldf; i += NT) PJ_A[i] = PJ_F[i];
     double b = l < n ? P.f[l] : 0.0;
     pj_sync<NW>();
-    bool singular = false;
-    for (int k = 0; k < n; ++k) {
-      // pivot: first row of maximal |a_ik|, i >= k (idamax)
-      double v = (l >= k && l < n) ? fabs(PJ_A[l * ldf + k]) : -1.0;
-      int idx = l;
-      for (int o = 1; o < 64; o <<= 1) {
-        const double v2 = __shfl_xor(v, o);
-        const int i2 = __shfl_xor(idx, o);
-        if (v2 > v || (v2 == v && i2 < idx)) {
-          v = v2;
-          idx = i2;
-        }
-      }
-      const int p = idx;
-      if (p != k) {  // swap rows k and p of A and of the right-hand side
-        if (NW > 1) pj_sync<NW>();  // every wave has read column k
-        for (int j = tid; j < n; j += NT) {
-          const double t = PJ_A[k * ldf + j];
-          PJ_A[k * ldf + j] = PJ_A[p * ldf + j];
-          PJ_A[p * ldf + j] = t;
-        }
-        const double bk = readlane_dbl(b, k), bp = readlane_dbl(b, p);
-        if (l == k) b = bp;
-        if (l == p) b = bk;
-      }
-      pj_sync<NW>();
-      const double akk = PJ_A[k * ldf + k];
-      if (akk == 0.0) singular = true;
-      const int m = n - 1 - k;
-      if (akk != 0.0 && m > 0) {
-        if (w0 && l > k && l < n)
-          PJ_A[l * ldf + k] = fabs(akk) >= DBL_MIN ? PJ_A[l * ldf + k] * (1.0 / akk) : PJ_A[l * ldf + k] / akk;
-        pj_sync<NW>();
-        // trailing update A[i][j] -= l_i A[k][j], i, j in (k, n): element e = (i - k - 1) m + (j - k - 1)
-        const int si = NT / m, sj = NT - si * m;
-        int i = tid / m, j = tid - i * m;
-        for (int e = tid; e < m * m; e += NT) {
-          const int gi = k + 1 + i, gj = k + 1 + j;
-          PJ_A[gi * ldf + gj] = PJ_A[gi * ldf + gj] - PJ_A[gi * ldf + k] * PJ_A[k * ldf + gj];
-          i += si;
-          j += sj;
-          if (j >= m) {
-            j -= m;
-            ++i;
-          }
-        }
-      }
-      pj_sync<NW>();
-    }
-    if (singular) {  // Julia's F \ f throws SingularException: the trajectory stops
+    if (lu_solve<NW>(PJ_A, n, ldf, b)) {  // Julia's F \ f throws SingularException: the trajectory stops
       if (tid == 0) P.status = 1;
       pj_sync<NW>();
       return;
-    }
-    // forward substitution (unit lower), then backward (upper), as dgetrs / dtrsm
-    for (int k = 0; k < n; ++k) {
-      const double bk = readlane_dbl(b, k);
-      if (bk != 0.0 && l > k && l < n) b = b - bk * PJ_A[l * ldf + k];
-    }
-    for (int k = n - 1; k >= 0; --k) {
-      const double ukk = PJ_A[k * ldf + k];
-      double bk = readlane_dbl(b, k);
-      if (bk != 0.0) {
-        bk = bk / ukk;
-        if (l == k) b = bk;
-        if (l < k) b = b - bk * PJ_A[l * ldf + k];
-      }
     }
     // s -= ds, updateMechanism!
     if (w0 && l < n) {
@@ -443,6 +460,116 @@ __device__ __forceinline__ double cstate_at(const PState& P, int i) {
   return P.wc[b][k - 10];
 }
 
+// ---- one variational-integrator step: ConstrainedDynamics 0.7.4 newton! (restated in gprx/vi.py,
+// which documents the equations): per body, with the current state (x1, q1, v1, w1) and the discrete
+// pose x2 = x1 + v1 dt, q2 = q1 wbar(w1) dt/2, Newton on s = (v2, w2 per body, lambda) for
+//     m ((v2 - v1)/dt + g e_z) - Gpos_x^T lambda = 0
+//     sq2 J w2 + w2 x J w2 - (sq1 J w1 - w1 x J w1) - Gpos_phi^T lambda = 0,  sq = sqrt(4/dt^2 - w.w)
+//     g(x3, q3) = 0,  x3 = x2 + v2 dt,  q3 = q2 wbar(w2) dt/2
+// Gpos = dg/d(x, phi) at pose 2 (phi: q -> q (1, phi)), fixed during the solve; the constraint rows'
+// velocity Jacobian is the projection's (subjoint).  One wave per state; the Newton matrix is
+// rebuilt in LDS every iteration and factored in place (lu_solve).
+// R(q) as gprx/vi.py rotmat (unit quaternions)
+__device__ __forceinline__ void rotm(const Qd& q, double (&R)[3][3]) {
+  const double w = q.w, x = q.x, y = q.y, z = q.z;
+  R[0][0] = w * w + x * x - y * y - z * z;
+  R[0][1] = 2.0 * (x * y - w * z);
+  R[0][2] = 2.0 * (x * z + w * y);
+  R[1][0] = 2.0 * (x * y + w * z);
+  R[1][1] = w * w - x * x + y * y - z * z;
+  R[1][2] = 2.0 * (y * z - w * x);
+  R[2][0] = 2.0 * (x * z - w * y);
+  R[2][1] = 2.0 * (y * z + w * x);
+  R[2][2] = w * w - x * x - y * y + z * z;
+}
+__device__ __forceinline__ void pose2(const PState& P, int b, double* x, Qd& q) {
+  if (b == 0) {
+    x[0] = x[1] = x[2] = 0.0;
+    q = Qd{1.0, 0.0, 0.0, 0.0};
+    return;
+  }
+  for (int k = 0; k < 3; ++k) x[k] = P.xk[b - 1][k];
+  q = ldq(P.qk[b - 1]);
+}
+// one sub-joint's rows of Gpos = dg/d(x_1, phi_1, ..., x_nb, phi_nb) at pose 2 (gprx/vi.py jac_phi)
+// into G (row-major, nd x n6); called by one lane
+__device__ void subjoint_pose_jac(const PState& P, const SubJoint& J, int n6, double* G) {
+  double xa[3], xb[3];
+  Qd qa, qb;
+  pose2(P, J.a, xa, qa);
+  pose2(P, J.b, xb, qb);
+  double Bx_b[3][3], Bp_b[3][3], Bx_a[3][3], Bp_a[3][3];  // the 3 x 3 blocks before C
+  if (J.kind == 0) {  // translational: g = C (R(qa)^T (xb + R(qb) pb - xa) - pa)
+    double Ra[3][3], Rb[3][3];
+    rotm(qa, Ra);
+    rotm(qb, Rb);
+    double y[3], u[3];
+    for (int i = 0; i < 3; ++i) y[i] = xb[i] + (Rb[i][0] * J.pb[0] + Rb[i][1] * J.pb[1] + Rb[i][2] * J.pb[2]) - xa[i];
+    for (int i = 0; i < 3; ++i) u[i] = Ra[0][i] * y[0] + Ra[1][i] * y[1] + Ra[2][i] * y[2];
+    const double spb[3][3] = {{0.0, -J.pb[2], J.pb[1]}, {J.pb[2], 0.0, -J.pb[0]}, {-J.pb[1], J.pb[0], 0.0}};
+    const double su[3][3] = {{0.0, -u[2], u[1]}, {u[2], 0.0, -u[0]}, {-u[1], u[0], 0.0}};
+    double RbS[3][3];  // R(qb) (-2 [pb]x)
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) RbS[i][j] = -2.0 * (Rb[i][0] * spb[0][j] + Rb[i][1] * spb[1][j] + Rb[i][2] * spb[2][j]);
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) {
+        Bx_b[i][j] = Ra[j][i];
+        Bp_b[i][j] = Ra[0][i] * RbS[0][j] + Ra[1][i] * RbS[1][j] + Ra[2][i] * RbS[2][j];
+        Bx_a[i][j] = -Ra[j][i];
+        Bp_a[i][j] = 2.0 * su[i][j];
+      }
+  } else {  // rotational: g = C Im(qa^-1 qb); d/dphi_b = Lmat(rq)[1:,1:], d/dphi_a = -Rmat(rq)[1:,1:]
+    const Qd r = qmul(qconj(qa), qb);
+    const double rv[3] = {r.x, r.y, r.z};
+    const double sr[3][3] = {{0.0, -rv[2], rv[1]}, {rv[2], 0.0, -rv[0]}, {-rv[1], rv[0], 0.0}};
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) {
+        Bx_b[i][j] = 0.0;
+        Bx_a[i][j] = 0.0;
+        Bp_b[i][j] = (i == j ? r.w : 0.0) + sr[i][j];
+        Bp_a[i][j] = -((i == j ? r.w : 0.0) - sr[i][j]);
+      }
+  }
+  for (int rr = 0; rr < J.rows; ++rr) {
+    double* g = G + (size_t)(J.row0 + rr) * n6;
+    for (int side = 0; side < 2; ++side) {
+      const int body = side ? J.a : J.b;
+      if (body == 0) continue;
+      const int c0 = 6 * (body - 1);
+      for (int j = 0; j < 3; ++j) {
+        double tx = 0.0, tp = 0.0;
+        for (int k = 0; k < 3; ++k) {
+          tx += J.C[rr][k] * (side ? Bx_a[k][j] : Bx_b[k][j]);
+          tp += J.C[rr][k] * (side ? Bp_a[k][j] : Bp_b[k][j]);
+        }
+        g[c0 + j] = tx;
+        g[c0 + 3 + j] = tp;
+      }
+    }
+  }
+}
+// the dynamics rows of the residual, lane j < n6: body b = j / 6
+__device__ __forceinline__ double vi_dyn_row(const PState& P, const MechDev& M, const double (*mom1)[3], const double* G,
+                                             int n6, int nd, double dt, double grav, int j) {
+  const int b = j / 6, c = j - 6 * b;
+  const double* v2 = P.s + 6 * b;
+  const double* w2 = v2 + 3;
+  double d;
+  if (c < 3) {
+    d = M.m[b] * ((v2[c] - P.vc[b][c]) / dt + (c == 2 ? grav : 0.0));
+  } else {
+    const int k = c - 3;
+    double Jw[3];
+    for (int i = 0; i < 3; ++i) Jw[i] = M.J[b][i][0] * w2[0] + M.J[b][i][1] * w2[1] + M.J[b][i][2] * w2[2];
+    const double sq2 = sqrt(4.0 / (dt * dt) - (w2[0] * w2[0] + w2[1] * w2[1] + w2[2] * w2[2]));
+    const double cr = k == 0 ? w2[1] * Jw[2] - w2[2] * Jw[1] : (k == 1 ? w2[2] * Jw[0] - w2[0] * Jw[2] : w2[0] * Jw[1] - w2[1] * Jw[0]);
+    d = (sq2 * Jw[k] + cr) - mom1[b][k];
+  }
+  double t = 0.0;
+  for (int r = 0; r < nd; ++r) t += G[(size_t)r * n6 + j] * P.s[n6 + r];
+  return d - t;
+}
+
 }  // namespace
 
 // ---- projectv! for T independent mechanism states: one wave each ------------------------------
@@ -459,6 +586,109 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
   if (l == 0) {
     a.iters_out[t] = P.it;
     a.status[t] = P.status;
+  }
+}
+
+// ---- one variational-integrator step for T independent states: one wave each --------------------
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_vi_step(ViArgs a) {
+  __shared__ PState P;
+  __shared__ double mom1[PJ_MAXB][3];
+  const int t = blockIdx.x, l = threadIdx.x;
+  const MechDev& M = a.mech;
+  const int nb = M.nb, nd = M.nd, n6 = 6 * nb, n = n6 + nd, ldf = n + 1;
+  const double dt = a.dt;
+  double* A = PJ_F;                         // the Newton matrix, rebuilt and factored each iteration
+  double* G = PJ_F + (size_t)n * ldf;       // Gpos (nd x n6), fixed
+  set_states(P, a.cs + (size_t)t * 13 * nb, nb, dt, l);
+  if (l < nb) {  // (sq1 I - [w1 x]) J w1; setsolution!: (v2, w2) start at the current velocities
+    const double* w1 = P.wc[l];
+    double Jw[3];
+    for (int i = 0; i < 3; ++i) Jw[i] = M.J[l][i][0] * w1[0] + M.J[l][i][1] * w1[1] + M.J[l][i][2] * w1[2];
+    const double sq1 = sqrt(4.0 / (dt * dt) - (w1[0] * w1[0] + w1[1] * w1[1] + w1[2] * w1[2]));
+    const double cr[3] = {w1[1] * Jw[2] - w1[2] * Jw[1], w1[2] * Jw[0] - w1[0] * Jw[2], w1[0] * Jw[1] - w1[1] * Jw[0]};
+    for (int i = 0; i < 3; ++i) {
+      mom1[l][i] = sq1 * Jw[i] - cr[i];
+      P.s[6 * l + i] = P.vc[l][i];
+      P.s[6 * l + 3 + i] = w1[i];
+    }
+  }
+  if (l >= n6 && l < n) P.s[l] = 0.0;
+  for (int i = l; i < nd * n6; i += 64) G[i] = 0.0;
+  __builtin_amdgcn_wave_barrier();
+  if (l < M.nsub) subjoint_pose_jac(P, M.sub[l], n6, G);
+  __builtin_amdgcn_wave_barrier();
+  int status = 1, it = 0;
+  for (int k = 1; k <= a.iters; ++k) {
+    // ---- the Newton matrix and the residual at the current solution
+    for (int i = l; i < n * ldf; i += 64) A[i] = 0.0;
+    __builtin_amdgcn_wave_barrier();
+    if (l < M.nsub) {
+      subjoint(P, M.sub[l], n6, ldf, dt, true, true, false);  // g(x3, q3) and dg/d(v2, w2)
+    } else if (l < M.nsub + 9 * nb) {  // d/dw2 [(sq2 I + [w2 x]) J w2] (gprx/vi.py)
+      const int e = l - M.nsub, b = e / 9, i = (e - 9 * b) / 3, kk = e - 9 * b - 3 * i;
+      const double* w2 = P.s + 6 * b + 3;
+      double Jw[3];
+      for (int q = 0; q < 3; ++q) Jw[q] = M.J[b][q][0] * w2[0] + M.J[b][q][1] * w2[1] + M.J[b][q][2] * w2[2];
+      const double sq2 = sqrt(4.0 / (dt * dt) - (w2[0] * w2[0] + w2[1] * w2[1] + w2[2] * w2[2]));
+      const double sw[3][3] = {{0.0, -w2[2], w2[1]}, {w2[2], 0.0, -w2[0]}, {-w2[1], w2[0], 0.0}};
+      const double sj[3][3] = {{0.0, -Jw[2], Jw[1]}, {Jw[2], 0.0, -Jw[0]}, {-Jw[1], Jw[0], 0.0}};
+      const double swJ = sw[i][0] * M.J[b][0][kk] + sw[i][1] * M.J[b][1][kk] + sw[i][2] * M.J[b][2][kk];
+      A[(6 * b + 3 + i) * ldf + 6 * b + 3 + kk] = ((sq2 * M.J[b][i][kk] + swJ) - sj[i][kk]) - Jw[i] * w2[kk] / sq2;
+    } else if (l < M.nsub + 12 * nb) {
+      const int e = l - M.nsub - 9 * nb, b = e / 3, c = e - 3 * b;
+      A[(6 * b + c) * ldf + 6 * b + c] = M.m[b] / dt;
+    }
+    for (int e = l; e < n6 * nd; e += 64) {  // -Gpos^T (upper right), -reg I (lower right)
+      const int j = e / nd, r = e - j * nd;
+      A[j * ldf + n6 + r] = -G[(size_t)r * n6 + j];
+    }
+    if (l < nd && a.reg != 0.0) A[(n6 + l) * ldf + n6 + l] = -a.reg;
+    __builtin_amdgcn_wave_barrier();
+    if (l < n6) P.f[l] = vi_dyn_row(P, M, mom1, G, n6, nd, dt, a.grav, l);
+    __builtin_amdgcn_wave_barrier();
+    // a system that is not finite (|w| beyond 2/dt: the reference's sqrt throws a DomainError) or is
+    // singular (SingularException) fails the state: its row is NaN
+    bool fin = l < n ? isfinite(P.f[l]) : true;
+    for (int i = l; i < n * ldf; i += 64) fin = fin && isfinite(A[i]);
+    if (__any(!fin)) {
+      status = 2;
+      break;
+    }
+    double bvec = l < n ? P.f[l] : 0.0;
+    if (lu_solve<1>(A, n, ldf, bvec) || __any(l < n && !isfinite(bvec))) {
+      status = 2;
+      break;
+    }
+    if (l < n) {
+      P.ds[l] = bvec;
+      P.s[l] = P.s[l] - bvec;
+    }
+    it = k;
+    __builtin_amdgcn_wave_barrier();
+    // ---- convergence: |f(s_new)| and |ds|
+    if (l < M.nsub) subjoint(P, M.sub[l], n6, ldf, dt, true, false, false);
+    __builtin_amdgcn_wave_barrier();
+    if (l < n6) P.f[l] = vi_dyn_row(P, M, mom1, G, n6, nd, dt, a.grav, l);
+    __builtin_amdgcn_wave_barrier();
+    const double fv = l < n ? P.f[l] : 0.0, dv = l < n ? P.ds[l] : 0.0;
+    const double nf = sqrt(wsum(fv * fv)), nds = sqrt(wsum(dv * dv));
+    if (nf < a.eps && nds < a.eps) {
+      status = 0;
+      break;
+    }
+  }
+  double* o = a.out + (size_t)t * 13 * nb;
+  for (int i = l; i < 13 * nb; i += 64) {
+    const int b = i / 13, k = i - 13 * b;
+    double v;
+    if (k < 3) v = P.xk[b][k];
+    else if (k < 7) v = P.qk[b][k - 3];
+    else v = P.s[6 * b + (k - 7)];  // v2 (7..9), w2 (10..12)
+    o[i] = status == 2 ? NAN : v;
+  }
+  if (l == 0) {
+    a.iters_out[t] = it;
+    a.status[t] = status;
   }
 }
 
@@ -543,6 +773,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 
 void launch_project(const ProjArgs& a, hipStream_t s) {
   if (a.T > 0) hipLaunchKernelGGL(k_project, dim3(a.T), dim3(64), pj_lds_bytes(a.mech.nb, a.mech.nd), s, a);
+}
+void launch_vi_step(const ViArgs& a, hipStream_t s) {
+  if (a.T <= 0) return;
+  const size_t n = 6 * (size_t)a.mech.nb + a.mech.nd;
+  const size_t lds = (n * (n + 1) + (size_t)a.mech.nd * 6 * a.mech.nb) * sizeof(double);
+  hipLaunchKernelGGL(k_vi_step, dim3(a.T), dim3(64), lds, s, a);
 }
 void launch_rollout_max(const RolloutMaxArgs& a, int dist_mode, hipStream_t s) {
   if (a.T <= 0) return;

@@ -82,6 +82,7 @@ SIGNATURES = {
     "gprx_gp_batch": (_vp, [_vp]),
     "gprx_rollout_min": (C.c_int, [_vp, C.c_int, C.c_int, C.c_double, C.c_int, C.c_int, C.POINTER(_vp), _ip, C.c_int,
                                    _ip, _dp, _dp]),
+    "gprx_vi_step": (C.c_int, [_vp, C.c_int, C.c_double, C.c_int, _dp, C.c_double, C.c_int, C.c_double, _dp, _ip, _ip]),
     "gprx_projectv": (C.c_int, [_vp, C.c_int, C.c_double, C.c_int, _dp, _dp, C.c_double, C.c_int, C.c_double, _dp, _ip,
                                 _ip]),
     "gprx_rollout_max": (C.c_int, [_vp, C.c_int, C.c_double, C.c_int, C.c_double, C.c_int, C.POINTER(_vp), _ip, C.c_int,

@@ -62,6 +62,32 @@ def projectv(mech: str, cstates, vw_pred, regularizer: float | None = None, newt
     return out, it, st
 
 
+def vi_step(mech: str, cstates, regularizer: float | None = None, newton_iter: int = 100, eps: float = 1e-10,
+            dt: float = DT, ctx: Context | None = None):
+    """One variational-integrator step (ConstrainedDynamics newton! after setstates!, the MeanDynamics
+    prior mean of src/mDynamics.jl:41-60) for T states on the device (k_vi_step, one wave each); the
+    same contract as the host restatement gprx.vi.vi_step: cstates (T, 13 nb) -> (solution CStates
+    (T, 13 nb) [x2, q2, v2, w2] per body, NaN rows for failed states; iterations (T,); status (T,):
+    0 converged, 1 not converged, 2 failed)."""
+    from . import vi
+
+    if mech not in MECH:
+        raise ValueError(f"Experiment {mech} not supported!")
+    nb = NBODIES[mech]
+    cs = np.ascontiguousarray(np.atleast_2d(cstates), dtype=np.float64)
+    T = cs.shape[0]
+    if cs.shape != (T, 13 * nb):
+        raise ValueError(f"cstates must be (T, {13 * nb})")
+    reg = vi.REGULARIZER[mech] if regularizer is None else float(regularizer)
+    ctx = ctx or _default_ctx()
+    out = np.empty((T, 13 * nb))
+    it = np.empty(T, dtype=np.int32)
+    st = np.empty(T, dtype=np.int32)
+    L.check(L.lib.gprx_vi_step(ctx.h, MECH[mech], float(dt), T, L.dptr(cs), reg, int(newton_iter), float(eps),
+                               L.dptr(out), L.iptr(it), L.iptr(st)), ctx.h)
+    return out, it, st
+
+
 def predictdynamics(mech: str, groups, start, steps: int, vw_indices, regularizer: float | None = None,
                     traj_group=None, dt: float = DT, ctx: Context | None = None):
     """predictdynamics(mechanism, gps, startobservation, steps, getvw; regularizer) for T

@@ -202,7 +202,16 @@ def main(argv=None):
     ap.add_argument("--time-limit", type=float, default=float("nan"), help="seconds per group call (NaN: none)")
     ap.add_argument("--out", default="gpurun_out/params_final_checkpoint.json")
     ap.add_argument("--rehearse", action="store_true", help="allow ranks to share GPUs (gloo control plane)")
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks, one per GPU; without a launcher N > 1 starts them itself (as bench.py does)")
     a = ap.parse_args(argv)
+    if a.gpus is not None:
+        if "WORLD_SIZE" not in os.environ and a.gpus > 1:  # parent: no GPU call has been made
+            import sys
+
+            raise SystemExit(shard.launch_ranks(os.path.abspath(sys.argv[0]), a.gpus, a.rehearse,
+                                                sys.argv[1:] if argv is None else list(argv), "search"))
+        shard.check_world(a.gpus, "search")
     world = shard.init_ranks(a.rehearse)
     t0 = time.perf_counter()
     res = run([e for e in a.experiments.split(",") if e], [int(s) for s in a.sizes.split(",") if s], a.trials,

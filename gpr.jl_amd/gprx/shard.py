@@ -53,6 +53,46 @@ def init_ranks(rehearse: bool = False) -> int:
     return world
 
 
+def launch_ranks(script: str, gpus: int, rehearse: bool, argv: list[str], tag: str = "gprx") -> int:
+    """`<script> --gpus N` (N > 1) started without a launcher: start N ranks, one per GPU, as a
+    torch.distributed.run child running the same script and arguments (the driver's own command
+    line), and return its exit code.  Call before this process touches a GPU (device_count() does
+    not initialise one on this image).  Fewer visible GPUs than N is an error (exit 2), not a silent
+    one-rank run; `rehearse` lets ranks share devices.  bench.py, sweep.py and search.py all start
+    their ranks through this."""
+    import socket
+    import subprocess
+    import sys
+
+    import torch
+
+    ndev = torch.cuda.device_count()
+    if ndev < gpus and not rehearse:
+        print(f"{tag}: --gpus {gpus} needs {gpus} visible GPUs, this host has {ndev} "
+              f"(--rehearse runs the ranks on shared devices, for a rehearsal only)", file=sys.stderr)
+        return 2
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), script, *argv]
+    print(f"{tag}: launching {gpus} ranks: {' '.join(cmd[1:6])} ...", file=sys.stderr, flush=True)
+    return subprocess.run(cmd).returncode
+
+
+def check_world(gpus: int, tag: str = "gprx") -> None:
+    """Under a launcher, `--gpus N` must equal WORLD_SIZE (exit 2 otherwise)."""
+    import os
+    import sys
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != gpus:
+        print(f"{tag}: --gpus {gpus} but WORLD_SIZE={world}: launch one rank per GPU "
+              f"(--gpus N without a launcher starts them itself)", file=sys.stderr)
+        raise SystemExit(2)
+
+
 def shard_trials(n_trials: int, rank: int, world: int) -> list[int]:
     """Trial-major round robin (the mapping core.jl's threads get, by jobid mod ngpu)."""
     return list(range(rank, n_trials, world))

@@ -3,6 +3,7 @@
 trial-sharded over one rank per GPU.  See gpr.jl_amd/gprx/sweep.py.
 
     python sweep.py [--trials 100 --max-evals 30 ...]                       # one GPU
+    python sweep.py --gpus 8                                                # 8 GPUs: starts its ranks
     python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \\
         --master-addr 127.0.0.1 --master-port 29500 sweep.py               # 8 GPUs (RCCL)
 """

@@ -94,3 +94,22 @@ def test_bench_refuses_more_ranks_than_gpus():
     p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2"], capture_output=True,
                        text=True, timeout=300, env=dict(env, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0"))
     assert p.returncode == 2 and "WORLD_SIZE=1" in p.stderr
+
+
+@pytest.mark.parametrize("script", ["sweep.py", "search.py"])
+def test_drivers_refuse_more_ranks_than_gpus(script):
+    """sweep.py and search.py start their ranks as bench.py does (shard.launch_ranks): `--gpus N`
+    with fewer visible GPUs than N exits 2 with a message, and a --gpus that disagrees with the
+    launcher's WORLD_SIZE exits 2 before any work."""
+    import torch
+
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("enough GPUs here: the launch would succeed")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, os.path.join(REPO, script), "--gpus", "2", "--trials", "1"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert p.returncode == 2, (p.returncode, p.stderr[-2000:])
+    assert "needs 2 visible GPUs" in p.stderr
+    p = subprocess.run([sys.executable, os.path.join(REPO, script), "--gpus", "2", "--trials", "1"], capture_output=True,
+                       text=True, timeout=300, env=dict(env, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0"))
+    assert p.returncode == 2 and "WORLD_SIZE=1" in p.stderr
