@@ -10,6 +10,11 @@ Prediction: predict_y(gp, obs) = μ(obs) + k*^T alpha -- in a rollout the physic
 step's states (here vectorised over all trajectories of all trials), the GP means in one batched
 device predict per step, the projection (maximal coordinates) on the device.
 
+The physics step runs on the device (k_vi_step through gprx.projection.vi_step, one wave per
+state); gprx.vi holds the host restatement it is tested against (tests/test_vi.py,
+tests/test_vi_device.py).  Every function takes `physics` (a callable (mech, states) -> (solution,
+iterations, status)) to run the same logic on another implementation, e.g. physics=vi.vi_step.
+
 Maximal coordinates (e.g. examples/maximal_coordinates/P2noise.jl:28-33): the CState input,
 getμ(vωindices) of the solution CState.  Minimal coordinates (e.g. minimal_coordinates/
 P2noise.jl:40-61): the experiment's xtransform builds the CState from (q, qdot) (velocities by the
@@ -100,14 +105,28 @@ def xtransform(mech: str, Xmin, usesin: bool) -> np.ndarray:
     raise ValueError(f"Experiment {mech} not supported!")
 
 
-def mean_max(mech: str, X) -> np.ndarray:
-    """μ(X) of the maximal-coordinate MD GPs: (G, N), output k = getμ(vωindices)[k]."""
-    return vi.mean_dynamics(mech, X, data.VW_INDICES[mech])
+def vi_step(mech: str, states, ctx=None):
+    """The product path's physics step: one variational-integrator step for every state on the device
+    (gprx.projection.vi_step -> gprx_vi_step -> k_vi_step)."""
+    from .projection import vi_step as device_step
+
+    return device_step(mech, states, ctx=ctx)
 
 
-def mean_min(mech: str, Xmin, usesin: bool) -> np.ndarray:
+def _physics(physics, ctx):
+    return physics if physics is not None else (lambda mech, S: vi_step(mech, S, ctx))
+
+
+def mean_max(mech: str, X, physics=None, ctx=None) -> np.ndarray:
+    """μ(X) of the maximal-coordinate MD GPs: (G, N), output k = getμ(vωindices)[k] of the solution
+    CState of each column (vi.mean_dynamics' contract)."""
+    sol, _, _ = _physics(physics, ctx)(mech, np.asarray(X, dtype=np.float64).T)
+    return sol[:, np.asarray(data.VW_INDICES[mech]) - 1].T.copy()
+
+
+def mean_min(mech: str, Xmin, usesin: bool, physics=None, ctx=None) -> np.ndarray:
     """μ(X) of the minimal-coordinate MD GPs: (nc, N)."""
-    sol, _, _ = vi.vi_step(mech, xtransform(mech, Xmin, usesin))
+    sol, _, _ = _physics(physics, ctx)(mech, xtransform(mech, Xmin, usesin))
     if mech == "P2":  # _getμ: (w1, w2 - w1) of the solution (minimal_coordinates/P2noise.jl:58)
         return np.stack([sol[:, 10], sol[:, 23] - sol[:, 10]])
     return sol[:, np.asarray(MIN_IDX[mech]) - 1].T.copy()
@@ -123,7 +142,19 @@ def _gp_means(rb, feats) -> np.ndarray:
     return mu.reshape(rb.n, rb.G, -1)
 
 
-def rollout_max(mech: str, rb, trials: list[int], starts, steps: int, regularizer=None, ctx=None):
+def simulate(mech: str, cstates, steps: int, physics=None, ctx=None):
+    """The physics-only baseline (vi.simulate's contract, examples/baseline.jl): steps + 1 physics
+    steps of every start state; (final CStates (T, 13 nb), OR of the per-step status flags (T,))."""
+    step = _physics(physics, ctx)
+    S = np.atleast_2d(np.asarray(cstates, dtype=np.float64))
+    bad = np.zeros(S.shape[0], dtype=np.int32)
+    for _ in range(steps + 1):
+        S, _, st = step(mech, S)
+        bad |= st
+    return S, bad
+
+
+def rollout_max(mech: str, rb, trials: list[int], starts, steps: int, regularizer=None, ctx=None, physics=None):
     """predictdynamics (examples/utils/predictdynamics.jl:7-22) with MeanDynamics GPs for the
     trajectories starts (n_local, M, 13 nb) of every local trial of rb: per step the GP means (one
     device predict for all trials), the physics means μ(obs) (all states at once), getvω, projectv!
@@ -143,7 +174,7 @@ def rollout_max(mech: str, rb, trials: list[int], starts, steps: int, regularize
         mu = _gp_means(rb, np.swapaxes(S, 1, 2))  # (n, G, M)
         mu[bad] = 0.0
         S[bad] = np.asarray(starts, dtype=np.float64)[bad]
-        sol, _, _ = vi.vi_step(mech, S.reshape(n * M, d))
+        sol, _, _ = _physics(physics, ctx)(mech, S.reshape(n * M, d))
         mu = mu + sol[:, idx].reshape(n, M, -1).transpose(0, 2, 1)
         vw_pred = getvw(mu.transpose(0, 2, 1), data.VW_INDICES[mech], nb)  # (n, M, 6 nb)
         vw, _, st = projectv(mech, S.reshape(n * M, d), vw_pred.reshape(n * M, -1), regularizer, ctx=ctx)
@@ -164,7 +195,7 @@ def _update(S, vw, nb):
     return np.concatenate([x2, q2, vw[..., 0:3], vw[..., 3:6]], axis=-1).reshape(n, M, d)
 
 
-def rollout_min(mech: str, rb, trials: list[int], starts, steps: int, usesin: bool):
+def rollout_min(mech: str, rb, trials: list[int], starts, steps: int, usesin: bool, physics=None, ctx=None):
     """predictdynamicsmin (examples/utils/predictdynamics.jl:30-102) with MeanDynamics GPs for the
     start observations starts (n_local, M, 2 nc) of every local trial of rb: per step the GP means
     at the previous state (one device predict for all trials) plus μ(obs), then the coordinates
@@ -183,7 +214,7 @@ def rollout_min(mech: str, rb, trials: list[int], starts, steps: int, usesin: bo
         feats = data.min_features(mech, obs.reshape(n * M, 2 * nc), usesin)  # (d, n M)
         mu = _gp_means(rb, feats.reshape(-1, n, M).transpose(1, 0, 2))  # (n, nc, M)
         mu[bad] = 0.0
-        mu = mu + mean_min(mech, feats, usesin).reshape(nc, n, M).transpose(1, 0, 2)
+        mu = mu + mean_min(mech, feats, usesin, physics, ctx).reshape(nc, n, M).transpose(1, 0, 2)
         rates = mu.transpose(0, 2, 1)  # (n, M, nc)
         q_old, qd_old = q_cur, rates
         q_cur = q_cur + rates * DT

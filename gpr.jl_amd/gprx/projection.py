@@ -125,6 +125,14 @@ def predictdynamics(mech: str, groups, start, steps: int, vw_indices, regularize
 
 
 def _default_ctx():
+    """The context of this process's current device (a rank bound to GPU LOCAL_RANK by
+    shard.init_ranks gets its own device's context)."""
     from .batch import default_context
 
-    return default_context()
+    try:
+        import torch
+
+        dev = torch.cuda.current_device() if torch.cuda.is_available() else 0
+    except ImportError:
+        dev = 0
+    return default_context(dev)

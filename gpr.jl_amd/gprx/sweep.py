@@ -24,9 +24,11 @@ Variants (all of noise.jl:72-85):
              simulationerror of the final CStates (position MSE)
     min_sin  as min with (sin, cos) angle features (experiment_*_mz_min_sin)
     vi       the physics-only baseline (noise.jl:72-75, examples/baseline.jl): the noisy test starts
-             simulated by the variational integrator alone (gprx.vi.simulate), no GP
+             simulated by the variational integrator alone (gprx.mdynamics.simulate: the device
+             step k_vi_step), no GP
     md_*     the same three with MeanDynamics GPs (experiment_*_md_*): the prior mean is one
-             variational-integrator step (gprx.vi / gprx.mdynamics), computed once per training
+             variational-integrator step (device k_vi_step via gprx.mdynamics; host restatement
+             gprx.vi), computed once per training
              set for the fit (y - mu(X) on the device) and at every rollout step's states; the
              GP means of a rollout step come from one batched device predict, the projection
              from the device
@@ -71,8 +73,8 @@ def _dist():
     return dist if dist.is_available() and dist.is_initialized() else None
 
 
-def local_trials(mech: str, N: int, variant: str, trial_ids, testsamples: int) -> list[dict]:
-    """The trials' GP inputs, built on the rank that owns them."""
+def local_trials(mech: str, N: int, variant: str, trial_ids, testsamples: int, ctx=None) -> list[dict]:
+    """The trials' GP inputs, built on the rank that owns them (MeanDynamics means on ctx's device)."""
     out = []
     md = variant.startswith("md_")
     base = variant[3:] if md else variant
@@ -83,7 +85,7 @@ def local_trials(mech: str, N: int, variant: str, trial_ids, testsamples: int) -
             th = data.theta0(mech, N, "MAX")
             d = dict(X=tr["X"], Y=tr["Y"], Xs=tr["Xs"], theta=np.tile(th, (tr["Y"].shape[0], 1)), trial=t, seed=seed)
             if md:  # MeanDynamics prior mean, once per training set (gprx.mdynamics)
-                d["mu"] = mdynamics.mean_max(mech, tr["X"])
+                d["mu"] = mdynamics.mean_max(mech, tr["X"], ctx=ctx)
         else:
             usesin = base == "min_sin"
             tr = data.make_trial_min(mech, N, testsamples, seed=seed, usesin=usesin)
@@ -91,7 +93,7 @@ def local_trials(mech: str, N: int, variant: str, trial_ids, testsamples: int) -
             d = dict(X=tr["X"], Y=tr["Y"], Xs=None, start=tr["start"], theta=np.tile(th, (tr["Y"].shape[0], 1)),
                      trial=t, seed=seed)
             if md:  # the rollout predicts at the test starts' features with the batch's test capacity
-                d["mu"] = mdynamics.mean_min(mech, tr["X"], usesin)
+                d["mu"] = mdynamics.mean_min(mech, tr["X"], usesin, ctx=ctx)
                 d["Xs"] = data.min_features(mech, tr["start"], usesin)
         if md:
             # a training column whose physics step fails (vi_step status 2, NaN) throws in the
@@ -114,7 +116,7 @@ def run_group(mech: str, N: int, variant: str, trial_ids, ctx, testsamples: int 
     from .optim import LBFGS, Options
 
     if trials is None:
-        trials = local_trials(mech, N, variant, trial_ids, testsamples)
+        trials = local_trials(mech, N, variant, trial_ids, testsamples, ctx)
     n = len(trials)
     if n == 0:
         return {}
@@ -168,7 +170,7 @@ def run_group(mech: str, N: int, variant: str, trial_ids, ctx, testsamples: int 
         good = [i for i in range(n) if np.all(ok_gp[i])]
         if good:
             starts = np.stack([trials[i]["start"] for i in range(n)])  # (n, M, 2 nc)
-            fin = mdynamics.rollout_min(mech, rb, good, starts, simsteps, usesin=variant == "md_min_sin")
+            fin = mdynamics.rollout_min(mech, rb, good, starts, simsteps, usesin=variant == "md_min_sin", ctx=ctx)
             for k, i in enumerate(good):
                 if np.isnan(fin[k]).any():  # a failed physics mean (vi_step status 2) throws in the reference
                     continue
@@ -201,11 +203,11 @@ def run_group(mech: str, N: int, variant: str, trial_ids, ctx, testsamples: int 
     return out
 
 
-def run_vi_baseline(mech: str, trial_ids, testsamples: int = 100, simsteps: int = 20) -> dict:
+def run_vi_baseline(mech: str, trial_ids, testsamples: int = 100, simsteps: int = 20, ctx=None) -> dict:
     """The pure variational-integrator baseline (noise.jl:72-75, examples/baseline.jl:3-16
     experimentVarInt): every noisy test start simulated for simsteps + 1 physics steps
-    (gprx.vi.simulate), error = simulationerror against the noise-free truth.  Host physics, no GP."""
-    from . import vi
+    (gprx.mdynamics.simulate, the device step), error = simulationerror against the noise-free
+    truth.  No GP."""
 
     n = len(trial_ids)
     err = np.full(n, math.inf)
@@ -216,7 +218,7 @@ def run_vi_baseline(mech: str, trial_ids, testsamples: int = 100, simsteps: int 
     # every test start of every local trial in one vectorised simulation (the states are
     # independent: each one's Newton iterates are those of a per-trial call)
     start = np.concatenate([data.make_trial(mech, 2, testsamples, seed=sd)["Xs"].T for sd in seeds])
-    fin, st = vi.simulate(mech, start, simsteps)
+    fin, st = mdynamics.simulate(mech, start, simsteps, ctx=ctx)
     for k, sd in enumerate(seeds):
         sl = slice(k * testsamples, (k + 1) * testsamples)
         # a test start whose physics step fails (vi_step status 2: the reference's DomainError /
@@ -246,7 +248,7 @@ def run(mechs=MECHS, sizes=SIZES, variants=VARIANTS, n_trials: int = 100, testsa
     for mech in mechs:
         if "vi" in variants:  # the pure variational-integrator baseline (noise.jl:72-75, idmod "VI")
             t0 = time.perf_counter()
-            r = run_vi_baseline(mech, mine, testsamples, simsteps)
+            r = run_vi_baseline(mech, mine, testsamples, simsteps, ctx)
             loc = {"kstep_mse": r["kstep_mse"].reshape(-1, 1), "failed": r["failed"].astype(np.float64).reshape(-1, 1),
                    "t": np.full((len(mine), 1), time.perf_counter() - t0)}
             g = shard.gather_results(loc, n_trials, lambda q: shard.shard_trials(n_trials, q, world), 0,

@@ -25,7 +25,7 @@ for k in ("mll", "grad", "mu", "var", "status", "info"):
 b.close()
 # small batch (B = 6 < 32): leaf size 1, the standalone diagonal kernel
 tr = data.make_trial("P2", 700, 16, seed=3)
-th = np.tile(data.theta0("P2", 700), (6, 1))
+th = np.tile(data.theta0("P2", 512), (6, 1))  # the config holds theta per experiment size
 b = gprx.GPBatch(6, tr["d"], 700, 16, ctx=ctx)
 b.set_train(tr["X"], tr["Y"])
 b.set_test(tr["Xs"])

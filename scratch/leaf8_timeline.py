@@ -1,0 +1,59 @@
+"""Timeline of the overlapped leaf (k_leaf8) on the bench workload, from a diagnostic build's
+stamps (scratch/devbuild.sh l8stamps -DGPRX_STAMPS -DGPRX_NODE8=0 -DGPRX_LAUUM_FWD -DGPRX_SLOTWG_N=0):
+
+    GPRX_LIB=scratch/var/libgprx_l8stamps.so python scratch/leaf8_timeline.py [trials]
+
+Events (s_memrealtime, 100 MHz; median over slots, us from the leaf's start): 0 start; diagonal
+wave: 1+2k / 2+2k start / end of tile k; task wave 0: 9+4k step k begins (tile k's inverse is
+ready), 10+4k after the chain tasks (tile k+1 handed over), 11+4k after the other TRSM tasks and
+inverse row k, 12+4k after the other SYRK tasks; 25 end.  Plus the diagonal routine's phases
+(diag_ts) per tile."""
+import ctypes as C
+import json
+import sys
+
+import numpy as np
+
+sys.path[:0] = ["/root/repo", "/root/repo/gpr.jl_amd"]
+import bench  # noqa: E402
+import gprx  # noqa: E402
+from gprx import _lib as L  # noqa: E402
+from gprx import shard  # noqa: E402
+
+trials = int(sys.argv[1]) if len(sys.argv) > 1 else 40
+f = L.lib.gprx_dbg_stamps
+f.restype = C.c_int
+f.argtypes = [C.c_int, C.c_void_p, C.c_longlong, C.c_int]
+trs, X, Y, T, XT = bench.make_workload(trials, 0, 1)
+rb = shard.RankBatch(trs, ctx=gprx.Context(0))
+TH = T.reshape(rb.n, bench.G, -1)
+for _ in range(3):
+    rb.evaluate(TH)
+assert f(2, None, 0, 1) == 0
+rb.evaluate(TH)
+n = 8 * 256 * 32
+nd = 8 * 256 * 4 * 16
+buf = np.zeros(n + nd, dtype=np.uint64)
+assert f(2, buf.ctypes.data, n + nd, 0) == 0
+ts = buf[:n].reshape(8, 256, 32).astype(np.float64)[:, : rb.n * bench.G]
+ds = buf[n:].reshape(8, 256, 4, 16).astype(np.float64)[:, : rb.n * bench.G]
+names = {0: "start", 25: "end"}
+for k in range(4):
+    names[1 + 2 * k], names[2 + 2 * k] = f"d{k}_start", f"d{k}_end"
+    names[9 + 4 * k], names[10 + 4 * k], names[11 + 4 * k], names[12 + 4 * k] = (
+        f"s{k}_begin", f"s{k}_chain_done", f"s{k}_trsm_inv_done", f"s{k}_syrk_done")
+out = {}
+for leaf in range(8):
+    t = ts[leaf]
+    if not (t[:, 0] > 0).all():
+        continue
+    row = {names[e]: round(float(np.median((t[:, e] - t[:, 0]) / 100.0)), 2) for e in sorted(names) if (t[:, e] > 0).all()}
+    out[f"leaf{leaf}"] = row
+    # the diagonal routine's phases per tile (durations, us): zero, then per P factor / TRSM / SYRK,
+    # inverse off-diagonal blocks, logdet
+    d = ds[leaf]
+    if (d[:, :, 15] > 0).all():
+        dur = np.median(np.diff(d, axis=2) / 100.0, axis=0)  # (4 tiles, 15)
+        lab = ["zero"] + [f"{x}{P}" for P in range(4) for x in ("fac", "trsm", "syrk")] + ["inv", "logdet"]
+        out[f"leaf{leaf}_diag"] = {f"tile{k}": dict(zip(lab, [round(float(v), 2) for v in dur[k]])) for k in range(4)}
+print(json.dumps(out, indent=1), flush=True)

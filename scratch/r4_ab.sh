@@ -8,7 +8,7 @@ for v in in-tree "$@"; do
   echo "== $v" >> gpurun_out/ab_bit.txt
   timeout -k 10 120 python scratch/bitcmp.py 8 >> gpurun_out/ab_bit.txt 2>&1
 done
-for i in 1 2; do
+for i in $(seq 1 ${REPS:-2}); do
   for v in in-tree "$@"; do
     if [ $v = in-tree ]; then unset GPRX_LIB; else export GPRX_LIB=scratch/var/libgprx_$v.so; fi
     timeout -k 10 150 python scratch/levels.py 40 3 > gpurun_out/ab_levels_${v}_$i.txt 2>&1

@@ -193,7 +193,7 @@ def test_fb_hyperparameter_optimise_n4096(ctx):
     b.close()
 
 
-@pytest.mark.parametrize("mech", ("P2", "CP"))
+@pytest.mark.parametrize("mech", ("P1", "P2", "CP", "FB"))
 def test_meandynamics_variants_against_oracle(ctx, mech):
     """noise.jl's experiment_*_md_max / _md_min / _md_min_sin (MeanDynamics GPs) through the product
     path (gprx.sweep.run_group -> gprx.mdynamics): mu(X) once per training set against the
@@ -201,6 +201,7 @@ def test_meandynamics_variants_against_oracle(ctx, mech):
     y - mu(X), and the rollouts (GP mean + physics mean per step; projectv! for maximal
     coordinates) against an oracle loop (oracle GP means, oracle VI, oracle projection)."""
     from gprx import data, mdynamics, sweep
+    from gprx.projection import REGULARIZER
     from gprx.rollout import final_cstate
     from oracle import projection_oracle as PO
     from oracle import vi_oracle as VO
@@ -246,7 +247,9 @@ def test_meandynamics_variants_against_oracle(ctx, mech):
                     s, _ = VO.vi_step(mech, obs)
                     return gp_mean(obs) + s[np.asarray(data.VW_INDICES[mech]) - 1]
 
-                ref, perr = PO.predictdynamics(mech, predict, starts[0, j], steps, data.VW_INDICES[mech])
+                # the experiments' projectv! regulariser (1e-10 for the four-bar, FBnoise.jl:43)
+                ref, perr = PO.predictdynamics(mech, predict, starts[0, j], steps, data.VW_INDICES[mech],
+                                               regularizer=REGULARIZER[mech])
                 np.testing.assert_allclose(fin[0, j], ref, rtol=0, atol=1e-7)
                 assert abs(pe[0, j] - perr) <= 1e-7 * max(1.0, perr)
         else:

@@ -101,11 +101,11 @@ def test_mean_functions_shapes_and_reference_rates(mech):
     """getμ(vωindices) of the maximal-coordinate experiments and the minimal-coordinate _getμ
     (P2: (w1, w2 - w1)): read from the same solution CState."""
     tr = data.make_trial(mech, 5, 0, seed=9)
-    mu = mdynamics.mean_max(mech, tr["X"])
+    mu = mdynamics.mean_max(mech, tr["X"], physics=vi.vi_step)  # the host step (no GPU here)
     sol, _, _ = vi.vi_step(mech, tr["X"].T)
     np.testing.assert_array_equal(mu, sol[:, np.asarray(data.VW_INDICES[mech]) - 1].T)
     tm = data.make_trial_min(mech, 5, 0, seed=9)
-    mm = mdynamics.mean_min(mech, tm["X"], False)
+    mm = mdynamics.mean_min(mech, tm["X"], False, physics=vi.vi_step)
     assert mm.shape == (len(data.MIN_COORDS[mech]), 5)
     s2, _, _ = vi.vi_step(mech, mdynamics.xtransform(mech, tm["X"], False))
     if mech == "P2":
