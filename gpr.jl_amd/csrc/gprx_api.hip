@@ -221,6 +221,18 @@ void factor_rec(gprx_ctx* c, hipStream_t st, const DevBatch& db, int o, int n, i
           [&] { gprx::launch_leaf(db, o, n, upd, st); }, n);
     return;
   }
+#ifndef GPRX_NODE8
+#define GPRX_NODE8 1
+#endif
+  if (GPRX_NODE8 && n == 8 && leaf == 4 && db.B >= 32) {  // top leaf + TRSM + SYRK + TT in one launch
+    const double m = 4 * T;
+    timed(c, st, "node8a", Bd * (2.0 * m * m * m / 3.0 + 3.0 * m * m * m), Bd * 8.0 * 4.0 * (2 * m) * (2 * m),
+          [&] { gprx::launch_node8(db, o, upd, st); }, n);
+    factor_rec(c, st, db, o + 4, 4, 1);
+    gprx::GemmGeom g{gprx::OP_LINV21, o, 4, 8, upd};
+    timed(c, st, "trtri_linv21", Bd * m * m * m, Bd * 8.0 * (3.0 * m * m + m * m / 2.0), [&] { gprx::launch_gemm(db, g, st); }, n);
+    return;
+  }
   if (n == 1) {
     timed(c, st, "diag", Bd * (T * T * T / 3.0 + T * T * T / 3.0), Bd * 8.0 * 3.0 * T * T,
           [&] { gprx::launch_diag(db, o, upd, st); });

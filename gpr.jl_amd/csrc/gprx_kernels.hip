@@ -676,8 +676,29 @@ __device__ __forceinline__ void leaf_ts(int o, int slot, int ev) {
   }
 }
 #define LEAF_TS(ev) leaf_ts(o, slot, ev)
+// k_leaf9 timeline (scratch/leaf8_timeline.py): lane 0 of the calling wave stamps event ev of
+// leaf o / 4 of this slot
+__device__ __forceinline__ void leaf9_ts(int o, int slot, int ev) {
+  if ((threadIdx.x & 63) == 0 && slot < 256) {
+    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    (&g_stamps[2][0][0])[((size_t)((o >> 2) & 7) * 256 + slot) * 32 + ev] = t;
+  }
+}
+#define L9_TS(ev) leaf9_ts(o, slot, ev)
+// the single-wave diagonal routine's internal events (after the leaf stamps in region 2)
+__device__ __forceinline__ void diag_ts(int jt, int slot, int ev) {
+  if ((threadIdx.x & 63) == 0 && slot < 256) {
+    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    (&g_stamps[2][0][0])[65536 + ((((size_t)((jt >> 2) & 7) * 256 + slot) * 4 + (jt & 3)) * 16) + ev] = t;
+  }
+}
+#define D_TS1(ev) diag_ts(jt, slot, ev)
 #else
+#define D_TS1(ev)
 #define LEAF_TS(ev)
+#define L9_TS(ev)
 #endif
 // ---- diagnostic build only (-DGPRX_GSTAMPS=op*100+n, scratch/gemm_timeline.py): per-wave
 // s_memrealtime of the GEMM launch of op at node size n: tile entry, core start, core end (loads
@@ -1254,21 +1275,28 @@ __constant__ int N8_PLAN[8][4] = {{0, 4, 24, -1},  {5, 8, 25, -1},  {9, 10, 26, 
 __host__ __device__ inline bool n8_plan(const GemmGeom& g1, const GemmGeom& g2) {
   return g1.op == OP_SYRK && g2.op == OP_TT && g1.n == 8 && g1.h == 4;
 }
+// units per slot of a launch (g2: the appended op; the n = 8 SYRK + TT launch: its fixed plan)
+template <bool PV>
+__device__ __forceinline__ int gemm_units(const DevBatch& db, const GemmGeom& g1, const GemmGeom& g2, int& T1) {
+  const bool plan = !PV && n8_plan(g1, g2);
+  T1 = plan ? 2 : op_units(g1, db.nt, db.mt);
+  return T1 + ((plan || g2.op == OP_NONE) ? 0 : op_units(g2, db.nt, db.mt));
+}
+// unit u of a slot on the four waves w = 0..3 that share it
 template <bool PV, int PM = PLAIN>
-__device__ __forceinline__ void gemm_body(const DevBatch& db, const GemmGeom& g1, const GemmGeom& g2) {
+__device__ __forceinline__ void gemm_unit(const DevBatch& db, const GemmGeom& g1, const GemmGeom& g2, int slot, int u, int w,
+                                          int T1) {
   int r0, c0, R, C, r02, c02, R2, C2;
   bool tri, tri2;
   op_rect(g1, db.nt, db.mt, r0, c0, R, C, tri);
   op_rect(g2, db.nt, db.mt, r02, c02, R2, C2, tri2);
   const bool plan = !PV && n8_plan(g1, g2);
-  const int T1 = plan ? 2 : op_units(g1, db.nt, db.mt), T2 = (plan || g2.op == OP_NONE) ? 0 : op_units(g2, db.nt, db.mt);
-  int slot, u, pr, pc;
-  if (!map_slot(db, T1 + T2, slot, u)) return;
+  int pr, pc;
   // the wave's tiles: the plan's list, or the unit (and its folded mirror) of the decomposition
   // below; ONE call site of gemm_tile (its cores are inlined once per kernel instance)
   int np = 1, pr2 = 0, pc2 = 0, sel0 = 0, w8 = 0, wr = 0, wc = 0;
   if (plan) {
-    w8 = 4 * u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    w8 = 4 * u + w;
     np = 4;
   } else {
     if (u >= T1) {
@@ -1279,7 +1307,6 @@ __device__ __forceinline__ void gemm_body(const DevBatch& db, const GemmGeom& g1
     const int op = (sel0 ? g2 : g1).op;  // block-uniform
     int UR, UC;
     unit_shape(op, UR, UC);
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     wr = w / UC;
     wc = w - wr * UC;
     if (tri) {  // lower-triangle tile 4u + w in row-major order
@@ -1327,6 +1354,15 @@ __device__ __forceinline__ void gemm_body(const DevBatch& db, const GemmGeom& g1
     // wave-uniform tile indices in SGPRs (the 64 x 64 core needs every VGPR)
     gemm_tile<PV, PM>(db, sel ? g2 : g1, slot, __builtin_amdgcn_readfirstlane(ti), __builtin_amdgcn_readfirstlane(tj), k);
   }
+}
+
+template <bool PV, int PM = PLAIN>
+__device__ __forceinline__ void gemm_body(const DevBatch& db, const GemmGeom& g1, const GemmGeom& g2) {
+  int T1;
+  const int T = gemm_units<PV>(db, g1, g2, T1);
+  int slot, u;
+  if (!map_slot(db, T, slot, u)) return;
+  gemm_unit<PV, PM>(db, g1, g2, slot, u, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), T1);
 }
 
 // 64 x 32 accumulator half-tile (mma_64x32 layout, columns 32 half ..) of sgn * L^-1[ti,tj]
@@ -1698,6 +1734,642 @@ __device__ __forceinline__ void leaf_body(const DevBatch& db, int o, int n, int 
 }
 
 __global__ __launch_bounds__(NTHR) void k_leaf(DevBatch db, int o, int n, int upd) { leaf_body(db, o, n, upd); }
+// ============================================================================================
+// Workgroup-local hand-offs of the fused leaf (k_leaf9): progress words and counter barriers in
+// LDS, polled by the waiting waves.  Every wait is bounded (2^24 polls, about half a second): a
+// hand-off that never comes ends the kernel with status GPRX_DEVICE_ERROR (3) for the slot instead
+// of a hung launch.
+// ============================================================================================
+__device__ __forceinline__ int lds_load(const int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+__device__ __forceinline__ void lds_publish(int* p, int v) {
+  // the writer's LDS and global stores are complete before the word changes
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if ((threadIdx.x & 63) == 0) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+constexpr int LW_SPIN = 1 << 24;
+__device__ __forceinline__ void lw_timeout(const DevBatch& db, int slot) {
+  if ((threadIdx.x & 63) == 0) db.status[slot] = 3;
+}
+__device__ __forceinline__ void lds_wait_gt(const int* p, int v, const DevBatch& db, int slot) {
+  for (int it = 0; lds_load(p) <= v; ++it) {
+    if (it > LW_SPIN) {
+      lw_timeout(db, slot);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+// ---- k_leaf9's diagonal wave: the diagonal routine of diag_tile_fast on one wave.  The 16 x 16
+// factor+inverse is an unscaled elimination (no square root inside the 16-step loop: the columns
+// are scaled by 1/sqrt(p_j) once at the end) with v_fmac_f64 taking the DPP row broadcast
+// directly, one instruction per update instead of a 64-bit broadcast move and an fma.  A single
+// wave issues one VALU instruction per ~4.5 cycles here, so the instruction count sets the time
+// (scratch/factbench: 4346 -> about 3500 cycles per 16 x 16 block).  The TRSM, SYRK and inverse
+// blocks of a panel are issued as one batch (all operand reads, then the MFMA chains interleaved,
+// then the stores) instead of block after block.  The inverse image's upper blocks are never
+// written (no reader touches them), and the tile's diagonal goes to ldiag[64] for the
+// log-determinant, which a task wave sums.
+// LDS writes of this wave complete and visible to its later reads (the compiler keeps the order)
+__device__ __forceinline__ void wave_sync() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+template <int M>
+__device__ __forceinline__ void fmac_bcast(double& acc, double src, double f) {
+  // acc += src[lane M of this row] * f.  A VALU write followed by a DPP read of the same register
+  // needs two wait states, which the compiler does not insert around inline assembly.  The only
+  // DPP source is a step's pivot column u[.][j], last written by the previous step's update for
+  // m = j; volatile keeps the updates in program order, so at least three updates (its X partner
+  // and the m = j+1 pair) separate that write from the first read.
+  asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(src), "v"(f), "i"(M));
+}
+template <int J, int M>
+__device__ __forceinline__ void fact_updates(double (&a)[16], double (&y)[16], double au, double fa, double fy) {
+  if constexpr (M < 16) {
+    fmac_bcast<M>(a[M], au, fa);  // a[m] -= u[m][j] u[i][j] / p_j   (fa = -u[i][j] / p_j)
+    fmac_bcast<M>(y[M], au, fy);  // W^-1[m][i] -= (u[m][j] / p_j) W^-1[j][i]   (fy = -W^-1[j][i] / p_j)
+    fact_updates<J, M + 1>(a, y, au, fa, fy);
+  }
+}
+template <int J>
+__device__ __forceinline__ double row_bcast_c(double v) { return __builtin_amdgcn_mov_dpp(v, 0x150 + J, 0xF, 0xF, true); }
+// Step J of the unscaled elimination A = U D^-1 U^T (U = L D^1/2, D = diag(p)): lane i holds row i
+// of U (a) and column i of W^-1 (y; W = U D^-1 unit lower) and d = its running diagonal, so the
+// next pivot is one DPP broadcast away and the step's critical path is the reciprocal of p_J (no
+// square root: the columns are scaled by 1/sqrt(p_J) once, after the last step).
+template <int J>
+__device__ __forceinline__ void fact_step(double (&a)[16], double (&y)[16], double& d, double& pv, int lr, int& fl) {
+  if constexpr (J < 16) {
+    const double au = a[J], yu = y[J];
+    const double p = row_bcast_c<J>(d);
+    const double pk = (p > 0.0) ? p : 1.0;
+    fl = (fl < 0 && !(p > 0.0)) ? J : fl;  // the first pivot <= 0 or NaN (continue with 1)
+    pv = (lr == J) ? pk : pv;
+    const double r0 = __builtin_amdgcn_rcp(pk);
+    const double e = fma(-pk, r0, 1.0);
+    const double ip = fma(r0, fma(e, e, e), r0);  // 1/p to the rounding level (error e^3)
+    d = fma(-au * au, ip, d);
+    fact_updates<J, J + 1>(a, y, au, -au * ip, -yu * ip);
+    fact_step<J + 1>(a, y, d, pv, lr, fl);
+  }
+}
+template <int J>
+__device__ __forceinline__ void fact_scale(double (&a)[16], double (&y)[16], double rl, double sl, int lr) {
+  if constexpr (J < 16) {
+    const double rJ = row_bcast_c<J>(rl);  // 1/sqrt(p_J)
+    a[J] = (lr > J) ? a[J] * rJ : (lr == J ? sl : 0.0);
+    y[J] = y[J] * rJ;
+    fact_scale<J + 1>(a, y, rl, sl, lr);
+  }
+}
+template <int P>
+__device__ __forceinline__ void w1_panel(double* T, const double* Xi, int lr, int lk) {
+  constexpr int NT = 3 - P;  // trailing blocks
+  if constexpr (NT > 0) {
+    constexpr int c0 = 16 * P;
+    // TRSM: A_iP <- A_iP Dinv^T, i = P+1 .. 3
+    double bv[4], av[NT][4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      bv[s] = Xi[(c0 + 4 * s + lk) * FS + c0 + lr];
+#pragma unroll
+      for (int i = 0; i < NT; ++i) av[i][s] = T[(c0 + 4 * s + lk) * FS + 16 * (P + 1 + i) + lr];
+    }
+    d4 acc[NT];
+#pragma unroll
+    for (int i = 0; i < NT; ++i) acc[i] = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int i = 0; i < NT; ++i) acc[i] = mfma(av[i][s], bv[s], acc[i]);
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) T[(c0 + lr) * FS + 16 * (P + 1 + i) + lk + 4 * q] = acc[i][q];
+    wave_sync();
+    // SYRK: A_ij -= A_iP A_jP^T for P < j <= i < 4
+    double pv[NT][4];
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) pv[i][s] = T[(c0 + 4 * s + lk) * FS + 16 * (P + 1 + i) + lr];
+    constexpr int NB = NT * (NT + 1) / 2;
+    d4 sacc[NB], old[NB];
+#pragma unroll
+    for (int b = 0, j = 0; j < NT; ++j)
+#pragma unroll
+      for (int i = j; i < NT; ++i, ++b) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) old[b][q] = T[(16 * (P + 1 + j) + lr) * FS + 16 * (P + 1 + i) + lk + 4 * q];
+        sacc[b] = (d4){0.0, 0.0, 0.0, 0.0};
+      }
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int b = 0, j = 0; j < NT; ++j)
+#pragma unroll
+        for (int i = j; i < NT; ++i, ++b) sacc[b] = mfma(pv[i][s], pv[j][s], sacc[b]);
+#pragma unroll
+    for (int b = 0, j = 0; j < NT; ++j)
+#pragma unroll
+      for (int i = j; i < NT; ++i, ++b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) T[(16 * (P + 1 + j) + lr) * FS + 16 * (P + 1 + i) + lk + 4 * q] = old[b][q] - sacc[b][q];
+    wave_sync();
+  }
+}
+// off-diagonal inverse blocks of sub-diagonal SD: X_ij = -Dinv_i sum_{k=j}^{i-1} L_ik X_kj, j = 0 .. 3-SD
+template <int SD>
+__device__ __forceinline__ void w1_inverse(const double* T, double* Xi, int lr, int lk) {
+  constexpr int NJ = 4 - SD;
+  d4 y[NJ], x[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) y[j] = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int kk = 0; kk < SD; ++kk) {
+    double av[NJ][4], bv[NJ][4];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int i = j + SD, kb = j + kk;
+        av[j][s] = T[(16 * kb + 4 * s + lk) * FS + 16 * i + lr];   // L_ik[lr][k]
+        bv[j][s] = Xi[(16 * j + lr) * FS + 16 * kb + 4 * s + lk];  // X_kj[k][lr]
+      }
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) y[j] = mfma(av[j][s], bv[j][s], y[j]);
+  }
+  double dv[NJ][4];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) dv[j][s] = Xi[(16 * (j + SD) + 4 * s + lk) * FS + 16 * (j + SD) + lr];  // Dinv_i[lr][4s+lk]
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) x[j] = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) x[j] = mfma(dv[j][s], y[j][s], x[j]);
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) Xi[(16 * j + lr) * FS + 16 * (j + SD) + lk + 4 * q] = -x[j][q];
+  wave_sync();
+}
+__device__ __forceinline__ void diag_w1(const DevBatch& db, int slot, int jt, double* T, double* Xi, double* ldiag) {
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  int fail = -1;
+  D_TS1(0);
+  for (int P = 0; P < 4; ++P) {
+    const int c0 = 16 * P;
+    double a[16], y[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      a[k] = T[(c0 + k) * FS + c0 + lr];
+      y[k] = (k == lr) ? 1.0 : 0.0;
+    }
+    double d = T[(c0 + lr) * FS + c0 + lr], pv = 1.0;
+    int fl = -1;
+    fact_step<0>(a, y, d, pv, lr, fl);
+    fl = __builtin_amdgcn_readfirstlane(fl);
+    if (fail < 0 && fl >= 0) fail = c0 + fl;
+    {
+      double sl, rl;
+      sqrt_rsqrt(pv, sl, rl);  // lane i: sqrt(p_i), 1/sqrt(p_i)
+      fact_scale<0>(a, y, rl, sl, lr);
+    }
+    if (l < 16) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) T[(c0 + k) * FS + c0 + l] = (k <= l) ? a[k] : 0.0;  // row l of L_PP
+      ldiag[c0 + l] = a[l];
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (l < 16) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) Xi[(c0 + l) * FS + c0 + r] = y[r];  // column l of Dinv
+    }
+    wave_sync();
+    D_TS1(1 + 2 * P);
+    switch (P) {
+      case 0: w1_panel<0>(T, Xi, lr, lk); break;
+      case 1: w1_panel<1>(T, Xi, lr, lk); break;
+      case 2: w1_panel<2>(T, Xi, lr, lk); break;
+      default: break;
+    }
+    D_TS1(2 + 2 * P);
+  }
+  w1_inverse<1>(T, Xi, lr, lk);
+  w1_inverse<2>(T, Xi, lr, lk);
+  w1_inverse<3>(T, Xi, lr, lk);
+  D_TS1(9);
+  if (fail >= 0 && l == 0 && db.status[slot] == 0) {
+    db.status[slot] = 1;
+    db.info[slot] = jt * TS + fail + 1;
+  }
+}
+
+struct Leaf9Sync {
+  int tk;          // task-wave barrier counter (monotonic, 7 per barrier)
+  int ch;          // chain-wave barrier counter (4 per barrier)
+  int diag_done;   // diagonal tiles factored and inverted
+  int tile_ready;  // diagonal tiles handed to wave 0 (tile 0 at the start)
+  int xfree;       // steps whose readers of dX[k & 1] are done
+};
+constexpr int L9_TW = 7;
+// Items go round the task waves, the three off the chain first (waves 5, 6, 7, then 1, 2, 3, 4);
+// the diagonal tile's four store quarters go to waves 4..7.
+constexpr int L9_HW = 7;
+__device__ __forceinline__ int l9_wave_of(int e) {
+  const int r = e % L9_HW;
+  return r < 3 ? 5 + r : (r < 6 ? r - 2 : 4);
+}
+__device__ __forceinline__ void ctr_barrier(int* ctr, int& gen, int nw, const DevBatch& db, int slot) {
+  gen += nw;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  for (int it = 0; lds_load(ctr) < gen; ++it) {
+    if (it > LW_SPIN) {
+      lw_timeout(db, slot);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+// acc[a] += sum_k Lx[16a + lk + 4q][k] b(k) for a triangular Lx (lower; LDS image Lx[c * FS + r]):
+// chunk s (k = 4s .. 4s + 3) reaches only the blocks a >= s / 4.  b[s] is lane (lr, lk)'s B operand
+// of chunk s.
+__device__ __forceinline__ void lmma_tri(d4 (&acc)[QM], const double* Lx, const double (&b)[16]) {
+  const int l = threadIdx.x & 63, llo = (l >> 4) * FS + (l & 15);
+#pragma unroll
+  for (int s = 0; s < 16; ++s)
+#pragma unroll
+    for (int a = s >> 2; a < QM; ++a) acc[a] = mfma(Lx[4 * s * FS + 16 * a + llo], b[s], acc[a]);
+}
+// Row-block core over global operands: acc[a] lane (lr, lk) reg q += sum_k M[16a + lk + 4q][k]
+// N[lr][k] (M, N column-major, K a multiple of 16).  Operands
+// one 16-deep stage ahead in registers, as mma_64x16 (whose MFMA operands are the other way round).
+__device__ __forceinline__ void frag16_load_rd(Frag16& f, const double* pa, const double* pb, size_t sa, size_t sb) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+#pragma unroll
+    for (int a = 0; a < QM; ++a) f.a[s][a] = pa[s * sa + 16 * a];
+    f.b[s] = pb[s * sb];
+  }
+}
+__device__ __forceinline__ void frag16_mma_rd(d4 (&acc)[QM], const Frag16& f) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int a = 0; a < QM; ++a) acc[a] = mfma(f.a[s][a], f.b[s], acc[a]);
+}
+__device__ __forceinline__ void mma_rd(d4 (&acc)[QM], const double* __restrict__ M, size_t ldm, const double* __restrict__ N,
+                                       size_t ldn, int K) {
+  const int nst = __builtin_amdgcn_readfirstlane(K >> 4);
+  if (nst <= 0) return;
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  const double* pa = M + lr + (size_t)lk * ldm;
+  const double* pb = N + lr + (size_t)lk * ldn;
+  const size_t sa = 4 * ldm, sb = 4 * ldn;
+  Frag16 f0, f1;
+  frag16_load_rd(f0, pa, pb, sa, sb);
+  int it = 0;
+  for (; it + 1 < nst; it += 2) {
+    __builtin_amdgcn_sched_barrier(0);
+    frag16_load_rd(f1, pa + (size_t)(it + 1) * 4 * sa, pb + (size_t)(it + 1) * 4 * sb, sa, sb);
+    frag16_mma_rd(acc, f0);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x020, 5, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const int n2 = (it + 2 < nst) ? it + 2 : it + 1;
+    frag16_load_rd(f0, pa + (size_t)n2 * 4 * sa, pb + (size_t)n2 * 4 * sb, sa, sb);
+    frag16_mma_rd(acc, f1);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x020, 5, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (it < nst) frag16_mma_rd(acc, f0);
+}
+__device__ __forceinline__ void acc_zero4(d4 (&acc)[QM]) {
+#pragma unroll
+  for (int a = 0; a < QM; ++a) acc[a] = (d4){0.0, 0.0, 0.0, 0.0};
+}
+
+__device__ __forceinline__ void leaf9_body(const DevBatch& db, int o, int upd) {
+  constexpr int n = 4;
+  extern __shared__ __attribute__((aligned(16))) double l9a[];
+  double* dT = l9a;                  // wave 0's tile image
+  double* dXb = dT + TS * FS;        // two inverse images
+  double* Tc = dXb + 2 * TS * FS;    // the chain's L(k+1,k), Tc[c * FS + r] = L[r][c]
+  double(*zq)[4][TS] = (double(*)[4][TS])(Tc + TS * FS);  // z partials: 6 off-diagonal tiles
+  double(*zqd)[4][TS] = zq + 6;                            // ... and the 4 diagonal tiles
+  double* ldiag = (double*)(zqd + 4);  // [2][64]: the diagonal of L_kk (log-determinant)
+  Leaf9Sync& sy = *(Leaf9Sync*)(ldiag + 2 * TS);
+  const int slot = blockIdx.x;
+  if (slot >= db.B || !slot_active(db, slot)) return;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  const size_t ld = db.ld, so = (size_t)slot * db.mat;
+  // 32-bit element offsets within a slot's matrix: a uniform part plus one of three lane parts
+  const int ldi = (int)ld;
+  const int lo = lk * ldi + lr;   // row + lr, column + lk
+  const int lo2 = lr * ldi + lk;  // row + lk, column + lr
+  const int llo = lk * FS + lr;   // LDS images: row + lr, column + lk
+  double* S = db.S + so;
+  const double* K0 = (upd ? db.S : db.K) + so;
+  double* Lw = db.Lw + so;
+  double* Li = db.Linv + so;
+  double* Mt = db.Mt + so;
+  const double* Y = db.Y + (size_t)slot * db.Npad;
+  {  // tile o into wave 0's image (all eight waves, all loads in flight first)
+    const double* A = K0 + (size_t)o * TS * ld + o * TS;
+    double v[TS * TS / (2 * NTHR)];
+#pragma unroll
+    for (int k = 0; k < TS * TS / (2 * NTHR); ++k) {
+      const int e = threadIdx.x + k * 2 * NTHR, r = e & 63, c = e >> 6;
+      v[k] = (r >= c) ? A[(size_t)c * ld + r] : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < TS * TS / (2 * NTHR); ++k) {
+      const int e = threadIdx.x + k * 2 * NTHR, r = e & 63, c = e >> 6;
+      dT[c * FS + r] = v[k];
+    }
+    if (threadIdx.x == 0) {
+      sy.tk = 0;
+      sy.ch = 0;
+      sy.diag_done = 0;
+      sy.tile_ready = 1;
+      sy.xfree = 0;
+    }
+  }
+  __syncthreads();
+  if (wave == 0) {  // ---- wave 0: the diagonal tiles
+    L9_TS(0);
+    for (int k = 0; k < n; ++k) {
+      lds_wait_gt(&sy.tile_ready, k, db, slot);
+      if (k >= 2) lds_wait_gt(&sy.xfree, k - 2, db, slot);  // step k-2's readers of dX[k & 1] done
+      L9_TS(1 + 2 * k);
+      diag_w1(db, slot, o + k, dT, dXb + (k & 1) * TS * FS, ldiag + (k & 1) * TS);
+      L9_TS(2 + 2 * k);
+      lds_publish(&sy.diag_done, k + 1);
+    }
+  } else {  // ---- the task waves
+    // chain quarter of this wave (-1: off the chain): waves 4, 1, 2, 3 -> 0, 1, 2, 3
+    const int cw = wave == 4 ? 0 : (wave <= 3 ? wave : -1);
+    const int cq = 16 * (cw < 0 ? 0 : cw);
+    int gen = 0, cgen = 0;
+    d4 yh[2][QM];       // held Y items (inverse row of the next step)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) acc_zero4(yh[h]);
+    // the chain's first operand of step k, A(o+k+1, o+k) rows cq.., staged in the idle inverse
+    // image dX[(k+1) & 1] (its step k-1 readers are past their barrier; wave 0 writes it again only
+    // after this chain hands tile k+1 over), Bs[c * FS + r] = A[r][c], this wave's rows only
+    auto preload = [&](int k) {
+      const double* Kc = k > 0 ? S : K0;
+      const int kk = o + k, k1 = kk + 1;
+      double* Bs = dXb + ((k + 1) & 1) * TS * FS;
+      double v[16];
+#pragma unroll
+      for (int s = 0; s < 16; ++s) v[s] = Kc[(kk * TS + 4 * s) * ldi + k1 * TS + cq + lo];
+#pragma unroll
+      for (int s = 0; s < 16; ++s) Bs[4 * s * FS + cq + llo] = v[s];
+    };
+    if (cw >= 0) preload(0);
+    for (int k = 0; k < n; ++k) {
+      const int kk = o + k;
+      const double* Kc = k > 0 ? S : K0;
+      const double* dX = dXb + (k & 1) * TS * FS;
+      // items of Y(k, j) held since the previous step: e = 4 j + c, on wave l9_wave_of(e), slot e / 7
+      const int nyp = 4 * k;  // Y(k, j), j < k
+      lds_wait_gt(&sy.diag_done, k, db, slot);
+      if (wave == 5) L9_TS(9 + 4 * k);
+      // ---- phase A: the chain; the held inverse items of row k; the diagonal tile's stores; the
+      //      other TRSMs of column k
+      if (k < n - 1 && cw >= 0) {
+        const int k1 = kk + 1;
+        d4 cp[QM];  // -A(k1, k1) rows cq.. (blocks a <= cw): loaded under the first product
+#pragma unroll
+        for (int a = 0; a < QM; ++a)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            cp[a][q] = -Kc[(k1 * TS + 16 * a + 4 * q) * ldi + k1 * TS + cq + lo];  // upper blocks: masked below
+        double bp[16];
+        {
+          const double* Bs = dXb + ((k + 1) & 1) * TS * FS;
+#pragma unroll
+          for (int s = 0; s < 16; ++s) bp[s] = Bs[4 * s * FS + cq + llo];
+        }
+        d4 u[QM];
+        acc_zero4(u);
+        lmma_tri(u, dX, bp);  // L(k1, kk) rows cq.. (transposed)
+#pragma unroll
+        for (int a = 0; a < QM; ++a)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            Lw[(kk * TS + 16 * a + 4 * q) * ldi + k1 * TS + cq + lo] = u[a][q];
+            Tc[(16 * a + 4 * q) * FS + cq + llo] = u[a][q];
+          }
+        ctr_barrier(&sy.ch, cgen, 4, db, slot);
+        // S(k1, k1) rows cq.. = A - L L^T: M = L from Tc, B operand = this wave's own rows of L
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+          const double b = u[s >> 2][s & 3];
+#pragma unroll
+          for (int a = 0; a < QM; ++a)
+            cp[a] = mfma(Tc[4 * s * FS + 16 * a + llo], b, cp[a]);
+        }
+#pragma unroll
+        for (int a = 0; a < QM; ++a)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int x = 16 * a + lk + 4 * q;  // column; row cq + lr
+            dT[(16 * a + 4 * q) * FS + cq + llo] = (cq + lr >= x) ? -cp[a][q] : 0.0;
+          }
+        ctr_barrier(&sy.ch, cgen, 4, db, slot);
+        if (cw == 0) lds_publish(&sy.tile_ready, k + 2);
+        if (wave == 4) L9_TS(10 + 4 * k);
+      }
+      // held items: X(k, j) = -Linv_kk Y(k, j), columns cq.. of tile (kk, o + j)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int e0 = h * L9_HW;
+        for (int e = e0; e < e0 + L9_HW && e < nyp; ++e) {
+          if (l9_wave_of(e) != wave) continue;
+          const int j = e >> 2, c = e & 3, tj = o + j, xq = 16 * c;
+          double b[16];
+#pragma unroll
+          for (int s = 0; s < 16; ++s) b[s] = yh[h][s >> 2][s & 3];
+          d4 x[QM];
+          acc_zero4(x);
+          lmma_tri(x, dX, b);
+          const double yv = Y[tj * TS + xq + lr];
+#pragma unroll
+          for (int a = 0; a < QM; ++a) {
+            double zt[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const double v = -x[a][q];  // Linv(kk, tj)[16a + lk + 4q][xq + lr]
+              Li[(tj * TS + xq) * ldi + kk * TS + 16 * a + 4 * q + lo2] = v;
+              Mt[(kk * TS + 16 * a + 4 * q) * ldi + tj * TS + xq + lo] = v;  // Mt(tj, kk)^T
+              zt[q] = row_sum16(v * yv);
+            }
+            if (lr == 0) {
+              const int kz = k * (k - 1) / 2 + j;
+#pragma unroll
+              for (int q = 0; q < 4; ++q) zq[kz][c][16 * a + lk + 4 * q] = zt[q];
+            }
+          }
+        }
+      }
+      // general phase-A items after the held ones: e = nyp.. : the diagonal tile's stores (4
+      // column quarters), then TRSM T(i, kk) rows (4 quarters per tile, i = kk + 2 ..)
+      {
+        const int nt1 = n - 2 - k > 0 ? n - 2 - k : 0;
+        const int na = 4 + 4 * nt1;
+        for (int e = 0; e < na; ++e) {
+          if ((e < 4 ? 4 + e : l9_wave_of(nyp + e - 4)) != wave) continue;
+          const int c = e & 3, xq = 16 * c;
+          if (e < 4) {  // columns xq.. of the diagonal tile: Linv, Mt = Linv^T, z partial
+            double* Lc = Li + (size_t)kk * TS * ld + kk * TS;
+            double* Mc = Mt + (size_t)kk * TS * ld + kk * TS;
+            const int r = l;
+            double t = 0.0;
+#pragma unroll 4
+            for (int cc = xq; cc < xq + 16; ++cc) {
+              const double xv = r >= cc ? dX[cc * FS + r] : 0.0;
+              Lc[(size_t)cc * ld + r] = xv;
+              Mc[(size_t)cc * ld + r] = (cc >= r) ? dX[r * FS + cc] : 0.0;
+              t = fma(xv, Y[kk * TS + cc], t);
+            }
+            zqd[k][c][r] = t;
+            if (c == 0) {  // the tile's log-determinant part from wave 0's copy of the diagonal
+              const double lsum = wave_sum(log(ldiag[(k & 1) * TS + l]));
+              if (l == 0) db.logdet_part[(size_t)slot * db.nt + kk] = lsum;
+            }
+          } else {  // T(ti, kk) rows xq..: L(ti, kk)[xq + lr][x] = sum_k A[xq + lr][k] Linv_kk[x][k]
+            const int ti = kk + 2 + ((e - 4) >> 2);
+            double b[16];
+#pragma unroll
+            for (int s = 0; s < 16; ++s) b[s] = Kc[(kk * TS + 4 * s) * ldi + ti * TS + xq + lo];
+            d4 u[QM];
+            acc_zero4(u);
+            lmma_tri(u, dX, b);
+#pragma unroll
+            for (int a = 0; a < QM; ++a)
+#pragma unroll
+              for (int q = 0; q < 4; ++q) Lw[(kk * TS + 16 * a + 4 * q) * ldi + ti * TS + xq + lo] = u[a][q];
+          }
+        }
+      }
+      ctr_barrier(&sy.tk, gen, L9_TW, db, slot);
+      if (wave == 5) {
+        lds_publish(&sy.xfree, k + 1);  // every reader of dX[k & 1] in step k is past the barrier
+        L9_TS(11 + 4 * k);
+      }
+      if (k == n - 1) break;
+      // ---- phase B: Y(k+1, j) for j <= k (held), then the SYRK rows of the trailing tiles
+      //      other than (kk+1, kk+1)
+      {
+        const int k1 = kk + 1;
+        const int ny = 4 * (k + 1);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int e0 = h * L9_HW;
+          for (int e = e0; e < e0 + L9_HW && e < ny; ++e) {
+            if (l9_wave_of(e) != wave) continue;
+            const int j = e >> 2, c = e & 3, tj = o + j, xq = 16 * c;
+            // Y(k1, tj)[:, xq..] = sum_{m=tj}^{kk} L(k1, m) Linv(m, tj): M = Lw row k1, N = Mt row tj
+            // (Linv(m, tj)^T); Linv(tj, tj)'s columns xq.. are zero above row xq: K starts at xq
+            acc_zero4(yh[h]);
+            mma_rd(yh[h], Lw + (size_t)(tj * TS + xq) * ld + k1 * TS, ld, Mt + (size_t)(tj * TS + xq) * ld + tj * TS + xq, ld,
+                   (k1 - tj) * TS - xq);
+          }
+        }
+        const int m = n - 1 - k;  // trailing tiles per edge
+        const int nsy = m * (m + 1) / 2 - 1;
+        for (int e = 0; e < 4 * nsy; ++e) {
+          if (l9_wave_of(ny + e) != wave) continue;
+          const int c = e & 3, xq = 16 * c;
+          int u = (e >> 2) + 1, cc = 0;  // lower trailing tile u (column-major), skipping (k1, k1)
+          while (u >= m - cc) {
+            u -= m - cc;
+            ++cc;
+          }
+          const int tj = k1 + cc, ti = tj + u;
+          // S(ti, tj) rows xq..: OUT[x][xq + lr] = S[xq + lr][x], M = L(tj, kk), N = L(ti, kk) rows xq..
+          // (a diagonal tile's blocks above the diagonal are formed and stored too: no reader uses them)
+          d4 acc[QM];
+#pragma unroll
+          for (int a = 0; a < QM; ++a)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[a][q] = -Kc[(tj * TS + 16 * a + 4 * q) * ldi + ti * TS + xq + lo];
+          mma_rd(acc, Lw + (size_t)kk * TS * ld + tj * TS, ld, Lw + (size_t)kk * TS * ld + ti * TS + xq, ld, TS);
+#pragma unroll
+          for (int a = 0; a < QM; ++a)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) S[(tj * TS + 16 * a + 4 * q) * ldi + ti * TS + xq + lo] = -acc[a][q];
+        }
+      }
+      ctr_barrier(&sy.tk, gen, L9_TW, db, slot);
+      if (wave == 5) L9_TS(12 + 4 * k);
+      if (cw >= 0 && k + 1 < n - 1) preload(k + 1);
+    }
+  }
+  __syncthreads();
+  if (wave == 0) L9_TS(25);
+  // z partials: the diagonal tiles' and the off-diagonal tiles' quarters summed in quarter order
+  for (int e = threadIdx.x; e < (n + 6) * TS; e += 2 * NTHR) {
+    const int t = e >> 6, r = e & 63;
+    int ti, tj;
+    double v;
+    if (t < n) {
+      ti = tj = o + t;
+      v = ((zqd[t][0][r] + zqd[t][1][r]) + zqd[t][2][r]) + zqd[t][3][r];
+    } else {
+      const int kz = t - n;
+      int k = 1;
+      while (k * (k + 1) / 2 <= kz) ++k;
+      ti = o + k;
+      tj = o + (kz - k * (k - 1) / 2);
+      v = ((zq[kz][0][r] + zq[kz][1][r]) + zq[kz][2][r]) + zq[kz][3][r];
+    }
+    zp_row(db, slot, 2 * tj)[ti * TS + r] = v;
+    zp_row(db, slot, 2 * tj + 1)[ti * TS + r] = 0.0;
+  }
+}
+constexpr size_t leaf9_lds_bytes() {
+  return (4 * TS * FS + 10 * 4 * TS + 2 * TS) * sizeof(double) + sizeof(Leaf9Sync);
+}
+__global__ __launch_bounds__(2 * NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_leaf9(DevBatch db, int o, int upd) {
+  leaf9_body(db, o, upd);
+}
+// The first half of an 8-tile recursion node (512 x 512) in one launch, one 8-wave workgroup per
+// slot: the top leaf (leaf9_body), TRSM and SYRK + TT -- three launches of the recursion with the
+// same tile work, a workgroup barrier between the phases.  The GEMM phases run the slot's units on
+// the two halves of the workgroup (gemm_unit).  (The bottom leaf and LINV21 stay launches of their
+// own: LINV21's epilogue beside the leaf spills.)
+__global__ __launch_bounds__(2 * NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_node9(DevBatch db, int o, int upd) {
+  const int slot = blockIdx.x;
+  if (slot >= db.B || !slot_active(db, slot)) return;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), half = wave >> 2, w = wave & 3;
+  const GemmGeom none{OP_NONE, 0, 0, 0};
+  leaf9_body(db, o, upd);
+  __syncthreads();
+  gemm_unit<false, REV_B>(db, GemmGeom{OP_TRSM, o, 4, 8, upd}, none, slot, half, w, 2);
+  __syncthreads();
+  gemm_unit<false, TRI_A_FIRST>(db, GemmGeom{OP_SYRK, o, 4, 8, upd}, GemmGeom{OP_TT, o, 4, 8, upd}, slot, half, w, 2);
+}
+
+
 
 // ============================================================================================
 // alpha = L^-T (L^-1 y).  phase 0: z = Linv y ; phase 1: alpha = Mt z.   grid = B * nt
@@ -2381,7 +3053,24 @@ void launch_diag(const DevBatch& b, int jt, int upd, hipStream_t s) {
   hipLaunchKernelGGL(k_diag_f, dim3(b.B), dim3(NTHR), 0, s, b, jt, upd);
 }
 void launch_leaf(const DevBatch& b, int o, int n, int upd, hipStream_t s) {
+  if (n == 4) {
+    static bool attr9 = false;
+    if (!attr9) {
+      attr9 = true;
+      (void)hipFuncSetAttribute((const void*)k_leaf9, hipFuncAttributeMaxDynamicSharedMemorySize, (int)leaf9_lds_bytes());
+    }
+    hipLaunchKernelGGL(k_leaf9, dim3(b.B), dim3(2 * NTHR), leaf9_lds_bytes(), s, b, o, upd);
+    return;
+  }
   hipLaunchKernelGGL(k_leaf, dim3(b.B), dim3(NTHR), 0, s, b, o, n, upd);
+}
+void launch_node8(const DevBatch& b, int o, int upd, hipStream_t s) {
+  static bool attr9 = false;
+  if (!attr9) {
+    attr9 = true;
+    (void)hipFuncSetAttribute((const void*)k_node9, hipFuncAttributeMaxDynamicSharedMemorySize, (int)leaf9_lds_bytes());
+  }
+  hipLaunchKernelGGL(k_node9, dim3(b.B), dim3(2 * NTHR), leaf9_lds_bytes(), s, b, o, upd);
 }
 void launch_gemm(const DevBatch& b, const GemmGeom& g, hipStream_t s, const GemmGeom& g2) {
   if (g.op != OP_PREDVAR && g.n <= b.small_n) {  // small node: pair units, 64 x 32 waves

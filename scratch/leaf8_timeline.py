@@ -52,7 +52,11 @@ for leaf in range(8):
     # the diagonal routine's phases per tile (durations, us): zero, then per P factor / TRSM / SYRK,
     # inverse off-diagonal blocks, logdet
     d = ds[leaf]
-    if (d[:, :, 15] > 0).all():
+    if (d[:, :, 9] > 0).all() and not (d[:, :, 15] > 0).any():  # k_leaf9's diag_w1: 0, factor/panel per P, inverse
+        dur = np.median(np.diff(d[:, :, :10], axis=2) / 100.0, axis=0)
+        lab = [f"{x}{P}" for P in range(4) for x in ("fac", "panel")] + ["inv"]
+        out[f"leaf{leaf}_diag"] = {f"tile{k}": dict(zip(lab, [round(float(v), 2) for v in dur[k]])) for k in range(4)}
+    elif (d[:, :, 15] > 0).all():
         dur = np.median(np.diff(d, axis=2) / 100.0, axis=0)  # (4 tiles, 15)
         lab = ["zero"] + [f"{x}{P}" for P in range(4) for x in ("fac", "trsm", "syrk")] + ["inv", "logdet"]
         out[f"leaf{leaf}_diag"] = {f"tile{k}": dict(zip(lab, [round(float(v), 2) for v in dur[k]])) for k in range(4)}
