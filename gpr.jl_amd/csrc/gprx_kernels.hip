@@ -854,11 +854,26 @@ __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
     for (int e = tid; e < d; e += NTHR) sc[e] = sqrt(P[e]);
     __syncthreads();
   }
-  for (int e = tid; e < TS * d; e += NTHR) {
-    const int r = e / d, p = e - r * d;
-    const double s = MODE == 1 ? sc[p] : 1.0;
-    xi[p * CS + r] = X[(size_t)i * TS * d + e] * s;
-    xj[p * CS + r] = X[(size_t)j * TS * d + e] * s;
+  {  // thread -> (dimension p = tid mod 32 + 32 k, rows tid / 32 + 8 m): no per-element division,
+     // 16 loads in flight per thread, coalesced over the 32 dimensions of a point row
+    const double* Xi = X + (size_t)i * TS * d;
+    const double* Xj = X + (size_t)j * TS * d;
+    for (int p = tid & 31; p < d; p += 32) {
+      const double s = MODE == 1 ? sc[p] : 1.0;
+      double vi[TS / 8], vj[TS / 8];
+#pragma unroll
+      for (int m = 0; m < TS / 8; ++m) {
+        const int r = (tid >> 5) + 8 * m;
+        vi[m] = Xi[r * d + p];
+        vj[m] = Xj[r * d + p];
+      }
+#pragma unroll
+      for (int m = 0; m < TS / 8; ++m) {
+        const int r = (tid >> 5) + 8 * m;
+        xi[p * CS + r] = vi[m] * s;
+        xj[p * CS + r] = vj[m] * s;
+      }
+    }
   }
   for (int e = tid; e < d + 3; e += NTHR) pw[e] = P[e];
   __syncthreads();
@@ -902,14 +917,11 @@ __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
     const int gj = j * TS + 4 * cb + b;
     double kv[4];
 #pragma unroll
-    for (int a = 0; a < 4; ++a) {
+    for (int a = 0; a < 4; ++a) {  // branch-free: padded points (finite coordinates) are selected away
       const int gi = i * TS + 4 * rb + a;
-      if (gi >= db.N || gj >= db.N) {
-        kv[a] = (gi == gj) ? 1.0 : 0.0;
-      } else {
-        const double fv = sf2 * exp_k(-rr[a][b] * 0.5, ek);
-        kv[a] = (gi == gj) ? fv + noise : fv;
-      }
+      const double fv = sf2 * exp_k(-rr[a][b] * 0.5, ek);
+      const bool pad = gi >= db.N || gj >= db.N;
+      kv[a] = (gi == gj) ? (pad ? 1.0 : fv + noise) : (pad ? 0.0 : fv);
     }
     const size_t off = (size_t)gj * db.ld + i * TS + 4 * rb;
     *(double2*)(K + off) = make_double2(kv[0], kv[1]);
