@@ -695,10 +695,20 @@ __device__ __forceinline__ void diag_ts(int jt, int slot, int ev) {
   }
 }
 #define D_TS1(ev) diag_ts(jt, slot, ev)
+// per-wave item events of the leaf's phase B (after the diagonal routine's events)
+__device__ __forceinline__ void wave_ts(int o, int slot, int ev) {
+  if ((threadIdx.x & 63) == 0 && slot < 256) {
+    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    (&g_stamps[2][0][0])[196608 + ((((size_t)((o >> 2) & 7) * 256 + slot) * 8 + (threadIdx.x >> 6)) * 32) + ev] = t;
+  }
+}
+#define W_TS(ev) wave_ts(o, slot, ev)
 #else
 #define D_TS1(ev)
 #define LEAF_TS(ev)
 #define L9_TS(ev)
+#define W_TS(ev)
 #endif
 // ---- diagnostic build only (-DGPRX_GSTAMPS=op*100+n, scratch/gemm_timeline.py): per-wave
 // s_memrealtime of the GEMM launch of op at node size n: tile entry, core start, core end (loads
@@ -2293,6 +2303,8 @@ __device__ __forceinline__ void leaf9_body(const DevBatch& db, int o, int upd) {
       {
         const int k1 = kk + 1;
         const int ny = 4 * (k + 1);
+        [[maybe_unused]] int nb = 0;
+        W_TS(8 * k);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const int e0 = h * L9_HW;
@@ -2304,6 +2316,7 @@ __device__ __forceinline__ void leaf9_body(const DevBatch& db, int o, int upd) {
             acc_zero4(yh[h]);
             mma_rd(yh[h], Lw + (size_t)(tj * TS + xq) * ld + k1 * TS, ld, Mt + (size_t)(tj * TS + xq) * ld + tj * TS + xq, ld,
                    (k1 - tj) * TS - xq);
+            W_TS(8 * k + 1 + (nb < 5 ? nb++ : 5));
           }
         }
         const int m = n - 1 - k;  // trailing tiles per edge
@@ -2329,7 +2342,9 @@ __device__ __forceinline__ void leaf9_body(const DevBatch& db, int o, int upd) {
           for (int a = 0; a < QM; ++a)
 #pragma unroll
             for (int q = 0; q < 4; ++q) S[(tj * TS + 16 * a + 4 * q) * ldi + ti * TS + xq + lo] = -acc[a][q];
+          W_TS(8 * k + 1 + (nb < 5 ? nb++ : 5));
         }
+        W_TS(8 * k + 7);
       }
       ctr_barrier(&sy.tk, gen, L9_TW, db, slot);
       if (wave == 5) L9_TS(12 + 4 * k);

@@ -1,0 +1,18 @@
+#!/bin/bash
+# Variant library from the whole scratch/dev source tree (kernels, API, header), for A/B runs that
+# change more than the kernels file: scratch/var/libgprx_NAME.so.  usage: scratch/devbuild.sh NAME [hipcc flags...]
+set -e
+cd "$(dirname "$0")"
+name=$1; shift
+mkdir -p var/o_$name
+H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off -w -Idev2"
+objs=""
+for f in dev2/gprx_kernels.hip dev2/gprx_lbfgs.hip dev2/gprx_projection.hip dev2/gprx_api.hip; do
+  o=var/o_$name/$(basename $f .hip).o
+  $H "$@" -c $f -o $o &
+  objs="$objs $o"
+done
+for j in $(jobs -p); do wait $j; done
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o var/libgprx_$name.so $objs ../gpr.jl_amd/lib/build_id.o
+rm -rf var/o_$name
+echo "scratch/var/libgprx_$name.so"

@@ -33,10 +33,12 @@ assert f(2, None, 0, 1) == 0
 rb.evaluate(TH)
 n = 8 * 256 * 32
 nd = 8 * 256 * 4 * 16
-buf = np.zeros(n + nd, dtype=np.uint64)
-assert f(2, buf.ctypes.data, n + nd, 0) == 0
+nw = 8 * 256 * 8 * 32
+buf = np.zeros(n + nd + nw, dtype=np.uint64)
+assert f(2, buf.ctypes.data, n + nd + nw, 0) == 0
+ws = buf[n + nd:].reshape(8, 256, 8, 32).astype(np.float64)[:, : rb.n * bench.G]
 ts = buf[:n].reshape(8, 256, 32).astype(np.float64)[:, : rb.n * bench.G]
-ds = buf[n:].reshape(8, 256, 4, 16).astype(np.float64)[:, : rb.n * bench.G]
+ds = buf[n:n + nd].reshape(8, 256, 4, 16).astype(np.float64)[:, : rb.n * bench.G]
 names = {0: "start", 25: "end"}
 for k in range(4):
     names[1 + 2 * k], names[2 + 2 * k] = f"d{k}_start", f"d{k}_end"
@@ -60,4 +62,16 @@ for leaf in range(8):
         dur = np.median(np.diff(d, axis=2) / 100.0, axis=0)  # (4 tiles, 15)
         lab = ["zero"] + [f"{x}{P}" for P in range(4) for x in ("fac", "trsm", "syrk")] + ["inv", "logdet"]
         out[f"leaf{leaf}_diag"] = {f"tile{k}": dict(zip(lab, [round(float(v), 2) for v in dur[k]])) for k in range(4)}
+    # phase B per wave (k_leaf9 W_TS): step k: 8k start, 8k+1.. after each item, 8k+7 end (us from leaf start)
+    w = ws[leaf]
+    if (w[:, 1:, 7] > 0).any():
+        ph = {}
+        for k in range(3):
+            for wv in range(1, 8):
+                t = w[:, wv, 8 * k: 8 * k + 8]
+                if not (t[:, 0] > 0).all():
+                    continue
+                rel = (t - ts[leaf][:, :1]) / 100.0
+                ph[f"s{k}_w{wv}"] = [round(float(np.median(rel[:, i])), 1) if (t[:, i] > 0).all() else None for i in range(8)]
+        out[f"leaf{leaf}_phaseB"] = ph
 print(json.dumps(out, indent=1), flush=True)
