@@ -128,28 +128,46 @@ __device__ __forceinline__ void sqrt_rsqrt(double p, double& s, double& r) {
   s = p * r;
   s = fma(0.5 * r, fma(-s, s, p), s);
 }
-// exp(x) for x <= 0 (the Gram's K and the gradient's recomputed Kf): Cody-Waite reduction
-// x = n ln2 + r (|r| <= ln2/2, r exact by fma), degree-13 Taylor polynomial (truncation
-// |r|^14/14! < 5e-18 relative, so about 1 ulp from the Horner rounding), ldexp; 0 below -745.
-// The coefficients live in a mutable device array that a kernel copies into registers once
+// exp(x) for x <= 0 (the Gram's K): x = (64 m + j) ln2/64 + r with |r| <= ln2/128 (Cody-Waite, r
+// exact by fma), 2^(j/64) from a 64-entry table the kernel stages in LDS (each entry correctly
+// rounded), a degree-5 Taylor polynomial (truncation |r|^6/720 < 4e-17 relative), ldexp by m; 0
+// below -745.  About 1.5 ulp, 16 VALU instructions against 21 for the degree-13 form without a
+// table.  The coefficients live in a mutable device array that a kernel copies into registers once
 // (uniform loads: SGPRs): with literal constants the compiler rematerialises every coefficient
-// per exp as two v_mov_b32 (14 per exp: 897 extra VALU instructions per gradient tile).
+// per exp as two v_mov_b32.
 struct ExpK {
-  double c[14];  // 1/13!, 1/12!, ..., 1/2, 1, 1
-  double l2e, ln2hi, ln2lo;
+  double c[6];         // 1/5!, 1/4!, 1/3!, 1/2, 1, 1
+  double k64, hi, lo;  // 64/ln2; ln2/64 split, hi with 32 significant bits (n hi exact, |n| < 2^21)
 };
-__device__ ExpK g_expk = {{1.6059043836821613e-10, 2.08767569878681e-09, 2.505210838544172e-08, 2.755731922398589e-07,
-                           2.7557319223985893e-06, 2.48015873015873e-05, 0.0001984126984126984, 0.001388888888888889,
-                           0.008333333333333333, 0.041666666666666664, 0.16666666666666666, 0.5, 1.0, 1.0},
-                          1.4426950408889634, 6.93147180369123816490e-01, 1.90821492927058770002e-10};
-__device__ __forceinline__ double exp_k(double x, const ExpK& k) {
-  const double n = rint(x * k.l2e);
-  double r = fma(-n, k.ln2hi, x);
-  r = fma(-n, k.ln2lo, r);
+__device__ ExpK g_expk = {{8.333333333333333e-03, 4.1666666666666664e-02, 0.16666666666666666, 0.5, 1.0, 1.0},
+                          92.33248261689366, 0.01083042469326756, 2.9815858269852933e-12};
+__device__ const double g_exp2tab[64] = {  // 2^(j/64), j = 0..63
+    1.0, 1.0108892860517005, 1.0218971486541166, 1.0330248790212284,
+    1.0442737824274138, 1.0556451783605572, 1.0671404006768237, 1.0787607977571199,
+    1.0905077326652577, 1.102382583307841, 1.1143867425958924, 1.1265216186082418,
+    1.1387886347566916, 1.1511892299529827, 1.1637248587775775, 1.1763969916502812,
+    1.189207115002721, 1.202156731452703, 1.215247359980469, 1.22848053610687,
+    1.241857812073484, 1.255380757024691, 1.2690509571917332, 1.2828700160787783,
+    1.2968395546510096, 1.3109612115247644, 1.3252366431597413, 1.339667524053303,
+    1.3542555469368927, 1.3690024229745905, 1.383909881963832, 1.3989796725383112,
+    1.4142135623730951, 1.42961333839197, 1.4451808069770467, 1.460917794180647,
+    1.4768261459394993, 1.4929077282912648, 1.5091644275934228, 1.5255981507445384,
+    1.5422108254079407, 1.559004400237837, 1.5759808451078865, 1.593142151342267,
+    1.6104903319492543, 1.6280274218573478, 1.645755478153965, 1.6636765803267364,
+    1.681792830507429, 1.7001063537185235, 1.718619298122478, 1.7373338352737062,
+    1.7562521603732995, 1.7753764925265212, 1.7947090750031072, 1.8142521755003989,
+    1.8340080864093424, 1.8539791250833855, 1.8741676341103, 1.8945759815869656,
+    1.9152065613971474, 1.9360617934922943, 1.9571441241754002, 1.978456026387951
+};
+__device__ __forceinline__ double exp_k(double x, const ExpK& k, const double* tab) {
+  const double n = rint(x * k.k64);
+  double r = fma(-n, k.hi, x);
+  r = fma(-n, k.lo, r);
   double p = k.c[0];
 #pragma unroll
-  for (int i = 1; i < 14; ++i) p = fma(p, r, k.c[i]);
-  return x < -745.0 ? 0.0 : ldexp(p, (int)n);
+  for (int i = 1; i < 6; ++i) p = fma(p, r, k.c[i]);
+  const int ni = (int)n;
+  return x < -745.0 ? 0.0 : ldexp(tab[ni & 63] * p, ni >> 6);
 }
 // 1/p by v_rcp_f64 + two Newton steps (|error| <= 1 ulp; the reference's dpotf2 scales by 1/ajj too)
 __device__ __forceinline__ double recip(double p) {
@@ -860,6 +878,7 @@ __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
   const double* X = db.X + (size_t)slot * db.Npad * d;
   const double* P = db.params + (size_t)slot * db.pst;
   double* sc = pw + DMAX + 4;  // direct mode: coordinates pre-scaled by 1/ell_p = sqrt(il2_p)
+  double* tab = sc + DMAX;     // exp_k's 2^(j/64) table
   if (MODE == 1) {
     for (int e = tid; e < d; e += NTHR) sc[e] = sqrt(P[e]);
     __syncthreads();
@@ -886,6 +905,7 @@ __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
     }
   }
   for (int e = tid; e < d + 3; e += NTHR) pw[e] = P[e];
+  if (tid < 64) tab[tid] = g_exp2tab[tid];
   __syncthreads();
   const double sf2 = pw[d], noise = pw[d + 1];
   const ExpK ek = g_expk;
@@ -929,7 +949,7 @@ __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
 #pragma unroll
     for (int a = 0; a < 4; ++a) {  // branch-free: padded points (finite coordinates) are selected away
       const int gi = i * TS + 4 * rb + a;
-      const double fv = sf2 * exp_k(-rr[a][b] * 0.5, ek);
+      const double fv = sf2 * exp_k(-rr[a][b] * 0.5, ek, tab);
       const bool pad = gi >= db.N || gj >= db.N;
       kv[a] = (gi == gj) ? (pad ? 1.0 : fv + noise) : (pad ? 0.0 : fv);
     }
@@ -3050,7 +3070,7 @@ __global__ __launch_bounds__(NT) void k_rollout(RolloutArgs a) {
 // ---------------------------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------------------------
-static size_t gram_lds(int d) { return (size_t)(2 * d * CS + 2 * DMAX + 4) * sizeof(double); }
+static size_t gram_lds(int d) { return (size_t)(2 * d * CS + 2 * DMAX + 4 + 64) * sizeof(double); }
 static size_t lauum_lds(const DevBatch& b) { return lauum_lds_dbl(b.xs, b.nimg) * sizeof(double); }
 static size_t cross_lds(int d) { return (size_t)(2 * d * CS + 2 * DMAX + 4) * sizeof(double); }
 
