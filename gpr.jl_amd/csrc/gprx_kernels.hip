@@ -942,6 +942,18 @@ __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
       }
   }
   double* K = db.K + (size_t)slot * db.mat;
+  if (i != j && (i + 1) * TS <= db.N) {  // off-diagonal tile inside N x N (block-uniform): no tests
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      double kv[4];
+#pragma unroll
+      for (int a = 0; a < 4; ++a) kv[a] = sf2 * exp_k(-rr[a][b] * 0.5, ek, tab);
+      const size_t off = (size_t)(j * TS + 4 * cb + b) * db.ld + i * TS + 4 * rb;
+      *(double2*)(K + off) = make_double2(kv[0], kv[1]);
+      *(double2*)(K + off + 2) = make_double2(kv[2], kv[3]);
+    }
+    return;
+  }
 #pragma unroll
   for (int b = 0; b < 4; ++b) {
     const int gj = j * TS + 4 * cb + b;
