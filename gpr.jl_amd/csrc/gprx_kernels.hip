@@ -2875,19 +2875,36 @@ __global__ __launch_bounds__(NTHR) void k_pred_cross(DevBatch db) {
   const double* Xq = db.Xs + (size_t)slot * db.Mpad * d;
   const double* P = db.params + (size_t)slot * db.pst;
   double* sc = pw + DMAX + 4;  // as k_gram
+  double* tab = sc + DMAX;
   if (MODE == 1) {
     for (int e = tid; e < d; e += NTHR) sc[e] = sqrt(P[e]);
     __syncthreads();
   }
-  for (int e = tid; e < TS * d; e += NTHR) {
-    const int r = e / d, p = e - r * d;
-    const double s = MODE == 1 ? sc[p] : 1.0;
-    xt[p * CS + r] = X[(size_t)ch * TS * d + e] * s;
-    xs[p * CS + r] = Xq[(size_t)mtile * TS * d + e] * s;
+  {  // as k_gram: no per-element division
+    const double* Xi = X + (size_t)ch * TS * d;
+    const double* Xj = Xq + (size_t)mtile * TS * d;
+    for (int p = tid & 31; p < d; p += 32) {
+      const double s = MODE == 1 ? sc[p] : 1.0;
+      double vi[TS / 8], vj[TS / 8];
+#pragma unroll
+      for (int m = 0; m < TS / 8; ++m) {
+        const int r = (tid >> 5) + 8 * m;
+        vi[m] = Xi[r * d + p];
+        vj[m] = Xj[r * d + p];
+      }
+#pragma unroll
+      for (int m = 0; m < TS / 8; ++m) {
+        const int r = (tid >> 5) + 8 * m;
+        xt[p * CS + r] = vi[m] * s;
+        xs[p * CS + r] = vj[m] * s;
+      }
+    }
   }
   for (int e = tid; e < d + 3; e += NTHR) pw[e] = P[e];
+  if (tid < 64) tab[tid] = g_exp2tab[tid];
   __syncthreads();
   const double sf2 = pw[d];
+  const ExpK ek = g_expk;
   // thread: 4 test points (4mb..) x 4 train points (4rb..)
   const int mb = tid & 15, rb = tid >> 4;
   double rr[4][4];
@@ -2922,6 +2939,7 @@ __global__ __launch_bounds__(NTHR) void k_pred_cross(DevBatch db) {
       }
   }
   double* KsT = db.KsT + (size_t)slot * db.Npad * db.Mpad;
+  const bool inner = (ch + 1) * TS <= db.N && (mtile + 1) * TS <= db.M;  // block-uniform
 #pragma unroll
   for (int a = 0; a < 4; ++a) {  // train point gt
     const int gt = ch * TS + 4 * rb + a;
@@ -2929,7 +2947,8 @@ __global__ __launch_bounds__(NTHR) void k_pred_cross(DevBatch db) {
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       const int gm = mtile * TS + 4 * mb + b;
-      kv[b] = (gt < db.N && gm < db.M) ? sf2 * exp(-rr[a][b] * 0.5) : 0.0;
+      const double fv = sf2 * exp_k(-rr[a][b] * 0.5, ek, tab);  // padded points: finite, selected away
+      kv[b] = (inner || (gt < db.N && gm < db.M)) ? fv : 0.0;
     }
     double* o = KsT + (size_t)gt * db.Mpad + mtile * TS + 4 * mb;
     *(double2*)o = make_double2(kv[0], kv[1]);
@@ -3084,7 +3103,7 @@ __global__ __launch_bounds__(NT) void k_rollout(RolloutArgs a) {
 // ---------------------------------------------------------------------------------------------
 static size_t gram_lds(int d) { return (size_t)(2 * d * CS + 2 * DMAX + 4 + 64) * sizeof(double); }
 static size_t lauum_lds(const DevBatch& b) { return lauum_lds_dbl(b.xs, b.nimg) * sizeof(double); }
-static size_t cross_lds(int d) { return (size_t)(2 * d * CS + 2 * DMAX + 4) * sizeof(double); }
+static size_t cross_lds(int d) { return (size_t)(2 * d * CS + 2 * DMAX + 4 + 64) * sizeof(double); }
 
 static void set_lds_limits() {
   static bool done = false;
