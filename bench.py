@@ -114,7 +114,8 @@ def pmc_field(stat: str, global_batch: int, fields):
 def roofline_parts(kern: dict, nprof: int, global_batch: int) -> dict:
     """The north star's two roofline figures beside the dominant kernel's: the Gram build against
     HBM (algorithmic bytes 8 (Npad^2/2 + Npad d) per slot: the lower tiles of K written, X read)
-    and the whole factorisation (leaf + TRSM + SYRK/TT + LINV21: Cholesky and L^-1, N^3/3 + N^3/3
+    and the whole factorisation (leaf, the fused 8-tile node halves, TRSM + SYRK/TT + LINV21:
+    Cholesky and L^-1, N^3/3 + N^3/3
     flops per slot) against the fp64 MFMA peak; the prediction-variance GEMM too.  Achieved =
     algorithmic work / HIP-event time on the library stream, per launch."""
     def part(names, bound):
@@ -147,7 +148,7 @@ def roofline_parts(kern: dict, nprof: int, global_batch: int) -> dict:
         gram["binding_limit"] = "valu"
         gram["valu_floor"] = pmc_field("gram", global_batch, ("valu_floor_ms", "valu_floor_frac", "clock_ghz_est"))
     return {"gram": gram,
-            "factorisation": part(["leaf", "diag", "potrf_trsm", "syrk_tt", "trtri_linv21"], "mfma"),
+            "factorisation": part(["leaf", "node8a", "diag", "potrf_trsm", "syrk_tt", "trtri_linv21"], "mfma"),
             "lauum_grad": part(["lauum_grad"], "mfma"),
             "pred_var": part(["pred_var"], "mfma")}
 
@@ -440,8 +441,8 @@ def main():
         for _ in range(nprof):
             rb.evaluate(TH)
         ctx.set_profiling(False)
-        names = ["gram", "leaf", "diag", "potrf_trsm", "syrk_tt", "trtri_linv21", "alpha", "lauum_grad",
-                 "finalize", "pred_cross", "pred_var", "pred_mu", "pred_final"]
+        names = ["gram", "leaf", "node8a", "diag", "potrf_trsm", "syrk_tt", "trtri_linv21", "alpha", "lauum_grad",
+                 "finalize", "pred_cross", "pred_var", "pred_final"]
         for nme in names:
             kern[nme] = ctx.kernel_stats(nme)
         dom = max(kern, key=lambda k: kern[k]["ms"])

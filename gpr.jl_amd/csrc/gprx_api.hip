@@ -268,7 +268,6 @@ void predict_var(gprx_ctx* c, hipStream_t st, const DevBatch& db) {
 }
 void predict_mean_final(gprx_ctx* c, hipStream_t st, const DevBatch& db) {
   const double N = db.N, M = db.M, B = db.B;
-  timed(c, st, "pred_mu", B * 2.0 * N * M, B * 8.0 * (N * db.Mpad + N), [&] { gprx::launch_pred_mu(db, st); });
   timed(c, st, "pred_final", B * 2.0 * db.nt * db.Mpad, B * 16.0 * db.nt * db.Mpad,
         [&] { gprx::launch_pred_final(db, st); });
 }

@@ -240,7 +240,6 @@ constexpr int LU = 24;
 int lauum_plan(int nt, int d, int* nunits, int* nimg, int* out);
 void launch_finalize(const DevBatch& b, int want_grad, hipStream_t s);
 void launch_pred_cross(const DevBatch& b, hipStream_t s);
-void launch_pred_mu(const DevBatch& b, hipStream_t s);
 void launch_pred_final(const DevBatch& b, hipStream_t s);
 void launch_rollout(const RolloutArgs& a, int dist_mode, hipStream_t s);
 void launch_lbfgs(const LbArgs& a, const DevBatch& db, int init, hipStream_t s);  // gprx_lbfgs.hip

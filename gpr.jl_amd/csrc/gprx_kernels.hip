@@ -128,46 +128,65 @@ __device__ __forceinline__ void sqrt_rsqrt(double p, double& s, double& r) {
   s = p * r;
   s = fma(0.5 * r, fma(-s, s, p), s);
 }
-// exp(x) for x <= 0 (the Gram's K): x = (64 m + j) ln2/64 + r with |r| <= ln2/128 (Cody-Waite, r
-// exact by fma), 2^(j/64) from a 64-entry table the kernel stages in LDS (each entry correctly
-// rounded), a degree-5 Taylor polynomial (truncation |r|^6/720 < 4e-17 relative), ldexp by m; 0
-// below -745.  About 1.5 ulp, 16 VALU instructions against 21 for the degree-13 form without a
-// table.  The coefficients live in a mutable device array that a kernel copies into registers once
+// exp(x) for x <= 0 (the Gram's K and the test cross-covariance): x = (64 m + j) ln2/64 + r with
+// |r| <= ln2/128 (Cody-Waite, r exact by fma), e^r = 1 + q with q a degree-5 Taylor polynomial
+// (truncation |r|^6/720 < 4e-17 relative), 2^(j/64) = hi_j + lo_j from a 64-entry table the kernel
+// stages in LDS, result hi + (hi q + lo) scaled by 2^m; 0 below -745.  About 0.51 ulp (the last
+// addition's rounding), 17 VALU instructions against 21 for the degree-13 form without a table.
+// The coefficients live in a mutable device array that a kernel copies into registers once
 // (uniform loads: SGPRs): with literal constants the compiler rematerialises every coefficient
 // per exp as two v_mov_b32.
 struct ExpK {
-  double c[6];         // 1/5!, 1/4!, 1/3!, 1/2, 1, 1
+  double c[4];         // 1/5!, 1/4!, 1/3!, 1/2
   double k64, hi, lo;  // 64/ln2; ln2/64 split, hi with 32 significant bits (n hi exact, |n| < 2^21)
 };
-__device__ ExpK g_expk = {{8.333333333333333e-03, 4.1666666666666664e-02, 0.16666666666666666, 0.5, 1.0, 1.0},
+__device__ ExpK g_expk = {{8.333333333333333e-03, 4.1666666666666664e-02, 0.16666666666666666, 0.5},
                           92.33248261689366, 0.01083042469326756, 2.9815858269852933e-12};
-__device__ const double g_exp2tab[64] = {  // 2^(j/64), j = 0..63
-    1.0, 1.0108892860517005, 1.0218971486541166, 1.0330248790212284,
-    1.0442737824274138, 1.0556451783605572, 1.0671404006768237, 1.0787607977571199,
-    1.0905077326652577, 1.102382583307841, 1.1143867425958924, 1.1265216186082418,
-    1.1387886347566916, 1.1511892299529827, 1.1637248587775775, 1.1763969916502812,
-    1.189207115002721, 1.202156731452703, 1.215247359980469, 1.22848053610687,
-    1.241857812073484, 1.255380757024691, 1.2690509571917332, 1.2828700160787783,
-    1.2968395546510096, 1.3109612115247644, 1.3252366431597413, 1.339667524053303,
-    1.3542555469368927, 1.3690024229745905, 1.383909881963832, 1.3989796725383112,
-    1.4142135623730951, 1.42961333839197, 1.4451808069770467, 1.460917794180647,
-    1.4768261459394993, 1.4929077282912648, 1.5091644275934228, 1.5255981507445384,
-    1.5422108254079407, 1.559004400237837, 1.5759808451078865, 1.593142151342267,
-    1.6104903319492543, 1.6280274218573478, 1.645755478153965, 1.6636765803267364,
-    1.681792830507429, 1.7001063537185235, 1.718619298122478, 1.7373338352737062,
-    1.7562521603732995, 1.7753764925265212, 1.7947090750031072, 1.8142521755003989,
-    1.8340080864093424, 1.8539791250833855, 1.8741676341103, 1.8945759815869656,
-    1.9152065613971474, 1.9360617934922943, 1.9571441241754002, 1.978456026387951
+__device__ const double g_exp2tab[128] = {  // (hi_j, lo_j): 2^(j/64) = hi_j + lo_j, j = 0..63
+    1.0, 0.0, 1.0108892860517005, -1.5234778603368577e-17,
+    1.0218971486541166, 5.109225028973444e-17, 1.0330248790212284, 7.600838874027088e-18,
+    1.0442737824274138, 8.551889705537965e-17, 1.0556451783605572, 1.759325738772092e-18,
+    1.0671404006768237, -7.899853966841582e-17, 1.0787607977571199, -6.656660436056593e-17,
+    1.0905077326652577, -3.046782079812471e-17, 1.102382583307841, 5.2660368715706944e-17,
+    1.1143867425958924, 1.0410278456845571e-16, 1.1265216186082418, 5.165856758795457e-17,
+    1.1387886347566916, 8.912812676025408e-17, 1.1511892299529827, 3.250710218863827e-17,
+    1.1637248587775775, 3.8292048369240935e-17, 1.1763969916502812, 5.554203254218079e-17,
+    1.189207115002721, 3.982015231465646e-17, 1.202156731452703, 6.644981499252301e-17,
+    1.215247359980469, -7.712630692681488e-17, 1.22848053610687, -1.89878163130253e-17,
+    1.241857812073484, 4.658027591836937e-17, 1.255380757024691, -6.7113898212968784e-18,
+    1.2690509571917332, 2.667932131342186e-18, 1.2828700160787783, 1.713594918243561e-17,
+    1.2968395546510096, 2.5382502794888315e-17, 1.3109612115247644, -7.181536135519454e-17,
+    1.3252366431597413, -2.8587312100388614e-17, 1.339667524053303, 8.927282594831732e-17,
+    1.3542555469368927, 7.70094837980299e-17, 1.3690024229745905, 9.593797919118849e-17,
+    1.383909881963832, -6.770511658794786e-17, 1.3989796725383112, -9.614213209051323e-17,
+    1.4142135623730951, -9.667293313452913e-17, 1.42961333839197, -1.2031642489053655e-17,
+    1.4451808069770467, -3.0237581349939873e-17, 1.460917794180647, -5.600377186075216e-17,
+    1.4768261459394993, -3.483994556892796e-17, 1.4929077282912648, 1.4192920154284036e-17,
+    1.5091644275934228, -1.016455327754295e-16, 1.5255981507445384, -1.1024941712342561e-16,
+    1.5422108254079407, 7.949834809697621e-17, 1.559004400237837, 3.7812070533575275e-17,
+    1.5759808451078865, -1.0136916471278304e-17, 1.593142151342267, -1.0094406542311964e-16,
+    1.6104903319492543, 2.4707192569797888e-17, 1.6280274218573478, -6.712955084707084e-17,
+    1.645755478153965, -1.0125679913674773e-16, 1.6636765803267364, 5.8909926967131e-17,
+    1.681792830507429, 8.199010020581497e-17, 1.7001063537185235, -8.0237193703977e-18,
+    1.718619298122478, -1.851380418263111e-17, 1.7373338352737062, 3.164389299292957e-17,
+    1.7562521603732995, 2.960140695448873e-17, 1.7753764925265212, 6.429731796556572e-17,
+    1.7947090750031072, 1.8227458427912087e-17, 1.8142521755003989, -9.969531538920349e-17,
+    1.8340080864093424, 3.283107224245627e-17, 1.8539791250833855, 9.761887490727594e-17,
+    1.8741676341103, -6.122763413004143e-17, 1.8945759815869656, 3.4034035352165297e-17,
+    1.9152065613971474, -1.0619946056195963e-16, 1.9360617934922943, 1.0332385960676326e-16,
+    1.9571441241754002, 8.960767791036668e-17, 1.978456026387951, 4.0388753109278167e-17
 };
 __device__ __forceinline__ double exp_k(double x, const ExpK& k, const double* tab) {
   const double n = rint(x * k.k64);
   double r = fma(-n, k.hi, x);
   r = fma(-n, k.lo, r);
-  double p = k.c[0];
+  double q = k.c[0];
 #pragma unroll
-  for (int i = 1; i < 6; ++i) p = fma(p, r, k.c[i]);
+  for (int i = 1; i < 4; ++i) q = fma(q, r, k.c[i]);
+  q = fma(q, r, 1.0) * r;  // e^r - 1
   const int ni = (int)n;
-  return x < -745.0 ? 0.0 : ldexp(tab[ni & 63] * p, ni >> 6);
+  const double2 t = *(const double2*)(tab + 2 * (ni & 63));
+  return x < -745.0 ? 0.0 : ldexp(t.x + fma(t.x, q, t.y), ni >> 6);
 }
 // 1/p by v_rcp_f64 + two Newton steps (|error| <= 1 ulp; the reference's dpotf2 scales by 1/ajj too)
 __device__ __forceinline__ double recip(double p) {
@@ -905,7 +924,7 @@ __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
     }
   }
   for (int e = tid; e < d + 3; e += NTHR) pw[e] = P[e];
-  if (tid < 64) tab[tid] = g_exp2tab[tid];
+  if (tid < 128) tab[tid] = g_exp2tab[tid];
   __syncthreads();
   const double sf2 = pw[d], noise = pw[d + 1];
   const ExpK ek = g_expk;
@@ -2901,7 +2920,7 @@ __global__ __launch_bounds__(NTHR) void k_pred_cross(DevBatch db) {
     }
   }
   for (int e = tid; e < d + 3; e += NTHR) pw[e] = P[e];
-  if (tid < 64) tab[tid] = g_exp2tab[tid];
+  if (tid < 128) tab[tid] = g_exp2tab[tid];
   __syncthreads();
   const double sf2 = pw[d];
   const ExpK ek = g_expk;
@@ -2939,44 +2958,42 @@ __global__ __launch_bounds__(NTHR) void k_pred_cross(DevBatch db) {
       }
   }
   double* KsT = db.KsT + (size_t)slot * db.Npad * db.Mpad;
+  const double* al = db.alpha + (size_t)slot * db.Npad;
   const bool inner = (ch + 1) * TS <= db.N && (mtile + 1) * TS <= db.M;  // block-uniform
+  double mp[4] = {0.0, 0.0, 0.0, 0.0};  // this thread's share of the partial means
 #pragma unroll
   for (int a = 0; a < 4; ++a) {  // train point gt
     const int gt = ch * TS + 4 * rb + a;
+    const double alt = al[gt];
     double kv[4];
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       const int gm = mtile * TS + 4 * mb + b;
       const double fv = sf2 * exp_k(-rr[a][b] * 0.5, ek, tab);  // padded points: finite, selected away
       kv[b] = (inner || (gt < db.N && gm < db.M)) ? fv : 0.0;
+      mp[b] = fma(kv[b], alt, mp[b]);
     }
     double* o = KsT + (size_t)gt * db.Mpad + mtile * TS + 4 * mb;
     *(double2*)o = make_double2(kv[0], kv[1]);
     *(double2*)(o + 2) = make_double2(kv[2], kv[3]);
   }
+  // the tile's partial means mu_part[ch][m] = sum_{t in tile ch} K*^T[t][m] alpha_t (k_pred_final adds
+  // the tiles): the 4 train points of the thread, then the 4 row groups of the wave, then the waves
+  double* mup = tab + 128;  // [4 waves][64 test points]
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    mp[b] += __shfl_xor(mp[b], 16);
+    mp[b] += __shfl_xor(mp[b], 32);
+  }
+  if ((tid & 63) < 16) {
+#pragma unroll
+    for (int b = 0; b < 4; ++b) mup[(tid >> 6) * TS + 4 * mb + b] = mp[b];
+  }
+  __syncthreads();
+  if (tid < TS)
+    db.mu_part[((size_t)slot * db.nt + ch) * db.Mpad + mtile * TS + tid] = ((mup[tid] + mup[TS + tid]) + mup[2 * TS + tid]) + mup[3 * TS + tid];
 }
 
-// Partial predictive means per training tile: mu_part[ch][m] = sum_{t in tile ch} K*^T[t][m] alpha_t.
-// grid = B * nt.  (Separate from k_pred_cross so that K*^T and the variance GEMM need only the
-// factorisation and can run beside alpha / the gradient on a second stream.)
-__global__ __launch_bounds__(NTHR) void k_pred_mu(DevBatch db) {
-  __shared__ double part[2][NTHR];
-  int slot, ch;
-  if (!map_slot(db, db.nt, slot, ch)) return;
-  const double* KsT = db.KsT + ((size_t)slot * db.Npad + (size_t)ch * TS) * db.Mpad;
-  const double* al = db.alpha + (size_t)slot * db.Npad + ch * TS;
-  const int tid = threadIdx.x, h = tid >> 7, mm = tid & 127;
-  for (int m0 = 0; m0 < db.Mpad; m0 += 128) {
-    const int m = m0 + mm;
-    double s = 0.0;
-    if (m < db.Mpad)
-      for (int t = 32 * h; t < 32 * h + 32; ++t) s = fma(KsT[(size_t)t * db.Mpad + m], al[t], s);
-    part[0][tid] = s;
-    __syncthreads();
-    if (h == 0 && m < db.Mpad) db.mu_part[((size_t)slot * db.nt + ch) * db.Mpad + m] = part[0][mm] + part[0][128 + mm];
-    __syncthreads();
-  }
-}
 
 __global__ __launch_bounds__(NTHR) void k_pred_final(DevBatch db) {
   const int slot = blockIdx.x;
@@ -3001,7 +3018,8 @@ __global__ __launch_bounds__(NTHR) void k_pred_final(DevBatch db) {
 // trajectory runs the whole rollout (the step chain is serial, so it is latency-bound; one launch
 // instead of steps x nc predict calls).  mu_g = sum_j sf2 exp(-r_j/2) alpha_j with r_j summed
 // exactly as k_pred_cross does (training point first, test point second), so a rollout step
-// reproduces gprx_batch_predict's mean up to the order of the final sum.  The state updates use
+// reproduces gprx_batch_predict's mean up to the exp's rounding (libm's here, k_pred_cross's table
+// exp_k, within 1.3 ulp) and the order of the final sum.  The state updates use
 // explicit round-to-nearest mul/add (no fma contraction), as the reference's Julia arithmetic.
 // ============================================================================================
 __device__ __forceinline__ double pick3(const double (&e)[3], int i) {
@@ -3101,9 +3119,9 @@ __global__ __launch_bounds__(NT) void k_rollout(RolloutArgs a) {
 // ---------------------------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------------------------
-static size_t gram_lds(int d) { return (size_t)(2 * d * CS + 2 * DMAX + 4 + 64) * sizeof(double); }
+static size_t gram_lds(int d) { return (size_t)(2 * d * CS + 2 * DMAX + 4 + 128) * sizeof(double); }
 static size_t lauum_lds(const DevBatch& b) { return lauum_lds_dbl(b.xs, b.nimg) * sizeof(double); }
-static size_t cross_lds(int d) { return (size_t)(2 * d * CS + 2 * DMAX + 4 + 64) * sizeof(double); }
+static size_t cross_lds(int d) { return (size_t)(2 * d * CS + 2 * DMAX + 4 + 128 + 4 * TS) * sizeof(double); }
 
 static void set_lds_limits() {
   static bool done = false;
@@ -3181,9 +3199,6 @@ void launch_pred_cross(const DevBatch& b, hipStream_t s) {
   const dim3 grid(grid_blocks(b.B, b.nt * b.mt));
   if (b.dist_mode == 0) hipLaunchKernelGGL(k_pred_cross<0>, grid, dim3(NTHR), cross_lds(b.d), s, b);
   else hipLaunchKernelGGL(k_pred_cross<1>, grid, dim3(NTHR), cross_lds(b.d), s, b);
-}
-void launch_pred_mu(const DevBatch& b, hipStream_t s) {
-  hipLaunchKernelGGL(k_pred_mu, dim3(grid_blocks(b.B, b.nt)), dim3(NTHR), 0, s, b);
 }
 void launch_pred_final(const DevBatch& b, hipStream_t s) {
   hipLaunchKernelGGL(k_pred_final, dim3(b.B), dim3(NTHR), 0, s, b);

@@ -30,7 +30,7 @@ ctx.set_profiling(False)
 names = ["gram", "leaf/n4", "leaf/n2", "diag", "node8a/n8"]
 for op in ("potrf_trsm", "syrk_tt", "trtri_linv21"):
     names += [f"{op}/n{n}" for n in (32, 16, 8, 4, 2)]
-names += ["alpha", "lauum_grad", "finalize", "pred_cross", "pred_var", "pred_mu", "pred_final"]
+names += ["alpha", "lauum_grad", "finalize", "pred_cross", "pred_var", "pred_final"]
 tot = 0.0
 for nm in names:
     try:
