@@ -1,6 +1,8 @@
 #!/bin/bash
 # Variant library from the whole scratch/dev source tree (kernels, API, header), for A/B runs that
-# change more than the kernels file: scratch/var/libgprx_NAME.so.  usage: scratch/devbuild.sh NAME [hipcc flags...]
+# change more than the kernels file: scratch/var/libgprx_NAME.so.  Populate the tree first
+# (mkdir -p scratch/dev && cp gpr.jl_amd/csrc/*.hip gpr.jl_amd/csrc/*.h scratch/dev/), edit it, then
+# usage: scratch/devbuild.sh NAME [hipcc flags...]
 set -e
 cd "$(dirname "$0")"
 name=$1; shift
