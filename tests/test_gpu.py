@@ -380,6 +380,36 @@ def test_factorisation_paths_match_golden(gprx, golden_dir, leaf, small_n):
         c.close()
 
 
+def test_fused_node_failure_isolated(gprx, ctx):
+    """The fused 8-tile node (k_node9: top leaf + TRSM + SYRK+TT, then k_leaf9 for the bottom leaf)
+    at B = 32, N = 512: a slot whose point p has NaN coordinates fails at pivot p + 1 (dpotf2's
+    first pivot that is not > 0), once in the top leaf (p = 100) and once in the bottom leaf
+    (p = 300); every other slot is bit-identical to a run without those slots' NaNs."""
+    from gprx import data
+
+    B, N = 32, 512
+    trs = [data.make_trial("P2", N, 1, seed=data.trial_seed("P2", t)) for t in range(B // 6 + 1)]
+    X = np.stack([trs[s // 6]["X"] for s in range(B)])
+    Y = np.stack([trs[s // 6]["Y"][s % 6] for s in range(B)])
+    th = np.tile(data.theta0("P2", N), (B, 1))
+    b = gprx.GPBatch(B, X.shape[1], N, 0, ctx=ctx)
+    b.set_train(X, Y)
+    ref = b.run(th, grad=True)
+    assert np.all(ref["status"] == 0)
+    Xn = X.copy()
+    Xn[5][:, 100] = np.nan
+    Xn[9][:, 300] = np.nan
+    b.set_train(Xn, Y)
+    r = b.run(th, grad=True)
+    assert r["status"][5] == 1 and r["info"][5] == 101
+    assert r["status"][9] == 1 and r["info"][9] == 301
+    keep = [s for s in range(B) if s not in (5, 9)]
+    assert np.all(r["status"][keep] == 0)
+    np.testing.assert_array_equal(r["mll"][keep], ref["mll"][keep])
+    np.testing.assert_array_equal(r["grad"][keep], ref["grad"][keep])
+    b.close()
+
+
 def test_production_path_b32_full_size(gprx, ctx):
     """The bench's configuration: B >= 32 slots (fused 256x256 leaves, folded 64x64 GEMM units,
     folded lauum jobs) at N=2048, d=26, M=100; three slots against the oracle, all slots finite
