@@ -186,7 +186,8 @@ __device__ __forceinline__ double exp_k(double x, const ExpK& k, const double* t
   q = fma(q, r, 1.0) * r;  // e^r - 1
   const int ni = (int)n;
   const double2 t = *(const double2*)(tab + 2 * (ni & 63));
-  return x < -745.0 ? 0.0 : ldexp(t.x + fma(t.x, q, t.y), ni >> 6);
+  const double v = ldexp(t.x + fma(t.x, q, t.y), ni >> 6);
+  return x < -745.0 ? 0.0 : v;  // a select, not a branch around the whole evaluation
 }
 // 1/p by v_rcp_f64 + two Newton steps (|error| <= 1 ulp; the reference's dpotf2 scales by 1/ajj too)
 __device__ __forceinline__ double recip(double p) {
@@ -876,6 +877,14 @@ __device__ __forceinline__ void acc_zero(d4 (&acc)[WM][WN]) {
 // a point in one bank (26-way conflicts on each ds_write_b64); 66 spreads them over the banks and
 // keeps the 16-B alignment of the inner loop's ds_read_b128.
 constexpr int CS = TS + 2;
+// Buffer resource over [base, base + bytes) (gfx9 word 3: raw, bounds-checked) and a 64-bit load
+// at byte offset voff (VGPR) + soff (SGPR): out-of-range reads return 0.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_rsrc(const void* base, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes, 0x00020000);
+}
+__device__ __forceinline__ double buffer_load_f64(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
+}
 template <int MODE>
 __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
@@ -904,16 +913,19 @@ __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
   }
   {  // thread -> (dimension p = tid mod 32 + 32 k, rows tid / 32 + 8 m): no per-element division,
      // 16 loads in flight per thread, coalesced over the 32 dimensions of a point row
-    const double* Xi = X + (size_t)i * TS * d;
-    const double* Xj = X + (size_t)j * TS * d;
+    // buffer loads: the lane's byte offset in a VGPR, the row step and tile base in SGPRs, so no
+    // per-load address arithmetic (64-bit global addresses cost 2-3 VALU per load here)
+    const __amdgpu_buffer_rsrc_t xr = buffer_rsrc(X, db.Npad * d * (int)sizeof(double));
+    const int bi = i * TS * d * (int)sizeof(double), bj = j * TS * d * (int)sizeof(double);
+    const int os = 8 * d * (int)sizeof(double);
     for (int p = tid & 31; p < d; p += 32) {
       const double s = MODE == 1 ? sc[p] : 1.0;
       double vi[TS / 8], vj[TS / 8];
+      const int o0 = ((tid >> 5) * d + p) * (int)sizeof(double);
 #pragma unroll
       for (int m = 0; m < TS / 8; ++m) {
-        const int r = (tid >> 5) + 8 * m;
-        vi[m] = Xi[r * d + p];
-        vj[m] = Xj[r * d + p];
+        vi[m] = buffer_load_f64(xr, o0, bi + m * os);
+        vj[m] = buffer_load_f64(xr, o0, bj + m * os);
       }
 #pragma unroll
       for (int m = 0; m < TS / 8; ++m) {
@@ -961,15 +973,17 @@ __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
       }
   }
   double* K = db.K + (size_t)slot * db.mat;
+  double* Kt = K + (size_t)j * TS * db.ld + i * TS;  // the tile (uniform); lane offsets 32-bit
+  const unsigned ldu = (unsigned)db.ld, lof = (unsigned)(4 * cb) * ldu + 4 * rb;
   if (i != j && (i + 1) * TS <= db.N) {  // off-diagonal tile inside N x N (block-uniform): no tests
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       double kv[4];
 #pragma unroll
       for (int a = 0; a < 4; ++a) kv[a] = sf2 * exp_k(-rr[a][b] * 0.5, ek, tab);
-      const size_t off = (size_t)(j * TS + 4 * cb + b) * db.ld + i * TS + 4 * rb;
-      *(double2*)(K + off) = make_double2(kv[0], kv[1]);
-      *(double2*)(K + off + 2) = make_double2(kv[2], kv[3]);
+      double* const Kb = Kt + lof + b * ldu;
+      *(double2*)(Kb) = make_double2(kv[0], kv[1]);
+      *(double2*)(Kb + 2) = make_double2(kv[2], kv[3]);
     }
     return;
   }
