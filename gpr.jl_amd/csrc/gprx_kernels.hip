@@ -885,13 +885,36 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_rsrc(const void* base, 
 __device__ __forceinline__ double buffer_load_f64(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
   return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
 }
+// sf2 e^x for x <= 0 (the Gram's K), exp_k's algorithm with three instructions fewer per element:
+// the table holds sf2 2^(j/64) as hi + lo (sf2 folded in at staging, exact to ~2^-106) at LDS
+// address 0 (no base add); n = rint(x 64/ln2) by the 1.5 2^52 shift (one fma and one add for a
+// multiply, a rint and a conversion; the fused product can pick the other neighbour when x 64/ln2
+// lies within an ulp of a half-integer, which leaves |r| <= ln2/128 + 2^-50 and the polynomial's
+// accuracy unchanged).  0 below -745, NaN propagates.
+__device__ __forceinline__ double exp_sf(double x, const ExpK& k, const double* tab0) {
+  constexpr double SH = 6755399441055744.0;  // 1.5 2^52
+  const double t = fma(x, k.k64, SH);
+  const double n = t - SH;
+  const int ni = (int)__double_as_longlong(t);
+  double r = fma(-n, k.hi, x);
+  r = fma(-n, k.lo, r);
+  double q = k.c[0];
+#pragma unroll
+  for (int i = 1; i < 4; ++i) q = fma(q, r, k.c[i]);
+  q = fma(q, r, 1.0) * r;  // e^r - 1
+  const double2 tt = *(const double2*)((const char*)tab0 + ((ni << 4) & 0x3f0));  // entry ni & 63
+  const double v = ldexp(tt.x + fma(tt.x, q, tt.y), ni >> 6);
+  return x < -745.0 ? 0.0 : v;
+}
 template <int MODE>
 __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
+  __shared__ __attribute__((aligned(16))) double tab[128];  // exp_sf's sf2 2^(j/64) table (static: a
+                                                            // known LDS address, no base add)
   const int d = db.d, tid = threadIdx.x;
   double* xi = sm;
-  double* xj = sm + d * CS;
-  double* pw = sm + 2 * d * CS;
+  double* xj = xi + d * CS;
+  double* pw = xj + d * CS;
   int slot, t, i = 0, j = 0;
   if (!map_slot(db, db.ntl, slot, t)) return;
   {  // t-th lower tile in column-major order
@@ -905,10 +928,11 @@ __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
   }
   const double* X = db.X + (size_t)slot * db.Npad * d;
   const double* P = db.params + (size_t)slot * db.pst;
-  double* sc = pw + DMAX + 4;  // direct mode: coordinates pre-scaled by 1/ell_p = sqrt(il2_p)
-  double* tab = sc + DMAX;     // exp_k's 2^(j/64) table
+  // direct mode: coordinates pre-scaled by 1/(sqrt(2) ell_p) = sqrt(il2_p / 2), so that the sums
+  // are r/2, the exponent's magnitude (0.5 il2_p is exact: as accurate as scaling by 1/ell_p)
+  double* sc = pw + DMAX + 4;
   if (MODE == 1) {
-    for (int e = tid; e < d; e += NTHR) sc[e] = sqrt(P[e]);
+    for (int e = tid; e < d; e += NTHR) sc[e] = sqrt(0.5 * P[e]);
     __syncthreads();
   }
   {  // thread -> (dimension p = tid mod 32 + 32 k, rows tid / 32 + 8 m): no per-element division,
@@ -936,9 +960,14 @@ __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
     }
   }
   for (int e = tid; e < d + 3; e += NTHR) pw[e] = P[e];
-  if (tid < 128) tab[tid] = g_exp2tab[tid];
+  if (tid < 64) {  // sf2 (hi_j + lo_j) as hi + lo: the product's rounding error by fma, plus sf2 lo_j
+    const double s2 = P[d], h = g_exp2tab[2 * tid], lo = g_exp2tab[2 * tid + 1];
+    const double th = s2 * h;
+    tab[2 * tid] = th;
+    tab[2 * tid + 1] = fma(s2, h, -th) + s2 * lo;
+  }
   __syncthreads();
-  const double sf2 = pw[d], noise = pw[d + 1];
+  const double noise = pw[d + 1];
   const ExpK ek = g_expk;
   const int rb = tid & 15, cb = tid >> 4;
   double rr[4][4];
@@ -980,7 +1009,7 @@ __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
     for (int b = 0; b < 4; ++b) {
       double kv[4];
 #pragma unroll
-      for (int a = 0; a < 4; ++a) kv[a] = sf2 * exp_k(-rr[a][b] * 0.5, ek, tab);
+      for (int a = 0; a < 4; ++a) kv[a] = exp_sf(MODE == 1 ? -rr[a][b] : -rr[a][b] * 0.5, ek, tab);
       double* const Kb = Kt + lof + b * ldu;
       *(double2*)(Kb) = make_double2(kv[0], kv[1]);
       *(double2*)(Kb + 2) = make_double2(kv[2], kv[3]);
@@ -994,7 +1023,7 @@ __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
 #pragma unroll
     for (int a = 0; a < 4; ++a) {  // branch-free: padded points (finite coordinates) are selected away
       const int gi = i * TS + 4 * rb + a;
-      const double fv = sf2 * exp_k(-rr[a][b] * 0.5, ek, tab);
+      const double fv = exp_sf(MODE == 1 ? -rr[a][b] : -rr[a][b] * 0.5, ek, tab);
       const bool pad = gi >= db.N || gj >= db.N;
       kv[a] = (gi == gj) ? (pad ? 1.0 : fv + noise) : (pad ? 0.0 : fv);
     }
@@ -3133,7 +3162,7 @@ __global__ __launch_bounds__(NT) void k_rollout(RolloutArgs a) {
 // ---------------------------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------------------------
-static size_t gram_lds(int d) { return (size_t)(2 * d * CS + 2 * DMAX + 4 + 128) * sizeof(double); }
+static size_t gram_lds(int d) { return (size_t)(2 * d * CS + 2 * DMAX + 4) * sizeof(double); }  // + k_gram's static table
 static size_t lauum_lds(const DevBatch& b) { return lauum_lds_dbl(b.xs, b.nimg) * sizeof(double); }
 static size_t cross_lds(int d) { return (size_t)(2 * d * CS + 2 * DMAX + 4 + 128 + 4 * TS) * sizeof(double); }
 
