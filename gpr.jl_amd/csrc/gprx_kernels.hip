@@ -128,11 +128,15 @@ __device__ __forceinline__ void sqrt_rsqrt(double p, double& s, double& r) {
   s = p * r;
   s = fma(0.5 * r, fma(-s, s, p), s);
 }
-// exp(x) for x <= 0 (the Gram's K and the test cross-covariance): x = (64 m + j) ln2/64 + r with
-// |r| <= ln2/128 (Cody-Waite, r exact by fma), e^r = 1 + q with q a degree-5 Taylor polynomial
-// (truncation |r|^6/720 < 4e-17 relative), 2^(j/64) = hi_j + lo_j from a 64-entry table the kernel
-// stages in LDS, result hi + (hi q + lo) scaled by 2^m; 0 below -745.  About 0.51 ulp (the last
-// addition's rounding), 17 VALU instructions against 21 for the degree-13 form without a table.
+// sf2 exp(x) for x <= 0 (the Gram's K and the test cross-covariance): x = (64 m + j) ln2/64 + r
+// with |r| <= ln2/128 + 2^-50 (Cody-Waite, r exact by fma), e^r = 1 + q with q a degree-5 Taylor
+// polynomial (truncation |r|^6/720 < 4e-17 relative), sf2 2^(j/64) = hi_j + lo_j from a 64-entry
+// table the kernel stages in static LDS (sf2 folded in at staging, the product's error by fma;
+// the static address makes the lookup two instructions), result hi + (hi q + lo) scaled by 2^m;
+// 0 below -745, NaN propagates.  n = rint(x 64/ln2) by the 1.5 2^52 shift: one fma and one add
+// for a multiply, a rint and a conversion (the fused product can pick the other neighbour when
+// x 64/ln2 lies within an ulp of a half-integer: |r| grows by 2^-50, the accuracy does not
+// change).  About 0.51 ulp; the guard is a select, not a branch around the evaluation.
 // The coefficients live in a mutable device array that a kernel copies into registers once
 // (uniform loads: SGPRs): with literal constants the compiler rematerialises every coefficient
 // per exp as two v_mov_b32.
@@ -176,18 +180,20 @@ __device__ const double g_exp2tab[128] = {  // (hi_j, lo_j): 2^(j/64) = hi_j + l
     1.9152065613971474, -1.0619946056195963e-16, 1.9360617934922943, 1.0332385960676326e-16,
     1.9571441241754002, 8.960767791036668e-17, 1.978456026387951, 4.0388753109278167e-17
 };
-__device__ __forceinline__ double exp_k(double x, const ExpK& k, const double* tab) {
-  const double n = rint(x * k.k64);
+__device__ __forceinline__ double exp_sf(double x, const ExpK& k, const double* tab0) {
+  constexpr double SH = 6755399441055744.0;  // 1.5 2^52
+  const double t = fma(x, k.k64, SH);
+  const double n = t - SH;
+  const int ni = (int)__double_as_longlong(t);
   double r = fma(-n, k.hi, x);
   r = fma(-n, k.lo, r);
   double q = k.c[0];
 #pragma unroll
   for (int i = 1; i < 4; ++i) q = fma(q, r, k.c[i]);
   q = fma(q, r, 1.0) * r;  // e^r - 1
-  const int ni = (int)n;
-  const double2 t = *(const double2*)(tab + 2 * (ni & 63));
-  const double v = ldexp(t.x + fma(t.x, q, t.y), ni >> 6);
-  return x < -745.0 ? 0.0 : v;  // a select, not a branch around the whole evaluation
+  const double2 tt = *(const double2*)((const char*)tab0 + ((ni << 4) & 0x3f0));  // entry ni & 63
+  const double v = ldexp(tt.x + fma(tt.x, q, tt.y), ni >> 6);
+  return x < -745.0 ? 0.0 : v;
 }
 // 1/p by v_rcp_f64 + two Newton steps (|error| <= 1 ulp; the reference's dpotf2 scales by 1/ajj too)
 __device__ __forceinline__ double recip(double p) {
@@ -884,27 +890,6 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_rsrc(const void* base, 
 }
 __device__ __forceinline__ double buffer_load_f64(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
   return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
-}
-// sf2 e^x for x <= 0 (the Gram's K), exp_k's algorithm with three instructions fewer per element:
-// the table holds sf2 2^(j/64) as hi + lo (sf2 folded in at staging, exact to ~2^-106) at LDS
-// address 0 (no base add); n = rint(x 64/ln2) by the 1.5 2^52 shift (one fma and one add for a
-// multiply, a rint and a conversion; the fused product can pick the other neighbour when x 64/ln2
-// lies within an ulp of a half-integer, which leaves |r| <= ln2/128 + 2^-50 and the polynomial's
-// accuracy unchanged).  0 below -745, NaN propagates.
-__device__ __forceinline__ double exp_sf(double x, const ExpK& k, const double* tab0) {
-  constexpr double SH = 6755399441055744.0;  // 1.5 2^52
-  const double t = fma(x, k.k64, SH);
-  const double n = t - SH;
-  const int ni = (int)__double_as_longlong(t);
-  double r = fma(-n, k.hi, x);
-  r = fma(-n, k.lo, r);
-  double q = k.c[0];
-#pragma unroll
-  for (int i = 1; i < 4; ++i) q = fma(q, r, k.c[i]);
-  q = fma(q, r, 1.0) * r;  // e^r - 1
-  const double2 tt = *(const double2*)((const char*)tab0 + ((ni << 4) & 0x3f0));  // entry ni & 63
-  const double v = ldexp(tt.x + fma(tt.x, q, tt.y), ni >> 6);
-  return x < -745.0 ? 0.0 : v;
 }
 template <int MODE>
 __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
@@ -2926,6 +2911,7 @@ __global__ __launch_bounds__(NTHR) void k_finalize(DevBatch db, int want_grad) {
 template <int MODE>
 __global__ __launch_bounds__(NTHR) void k_pred_cross(DevBatch db) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
+  __shared__ __attribute__((aligned(16))) double tab[128];  // exp_sf's table, as k_gram
   const int d = db.d, tid = threadIdx.x;
   double* xt = sm;
   double* xs = sm + d * CS;
@@ -2936,23 +2922,24 @@ __global__ __launch_bounds__(NTHR) void k_pred_cross(DevBatch db) {
   const double* X = db.X + (size_t)slot * db.Npad * d;
   const double* Xq = db.Xs + (size_t)slot * db.Mpad * d;
   const double* P = db.params + (size_t)slot * db.pst;
-  double* sc = pw + DMAX + 4;  // as k_gram
-  double* tab = sc + DMAX;
+  double* sc = pw + DMAX + 4;  // as k_gram (sqrt(il2 / 2): the sums are r/2)
   if (MODE == 1) {
-    for (int e = tid; e < d; e += NTHR) sc[e] = sqrt(P[e]);
+    for (int e = tid; e < d; e += NTHR) sc[e] = sqrt(0.5 * P[e]);
     __syncthreads();
   }
-  {  // as k_gram: no per-element division
-    const double* Xi = X + (size_t)ch * TS * d;
-    const double* Xj = Xq + (size_t)mtile * TS * d;
+  {  // as k_gram: no per-element division, buffer loads
+    const __amdgpu_buffer_rsrc_t xr = buffer_rsrc(X, db.Npad * d * (int)sizeof(double));
+    const __amdgpu_buffer_rsrc_t qr = buffer_rsrc(Xq, db.Mpad * d * (int)sizeof(double));
+    const int bi = ch * TS * d * (int)sizeof(double), bj = mtile * TS * d * (int)sizeof(double);
+    const int os = 8 * d * (int)sizeof(double);
     for (int p = tid & 31; p < d; p += 32) {
       const double s = MODE == 1 ? sc[p] : 1.0;
       double vi[TS / 8], vj[TS / 8];
+      const int o0 = ((tid >> 5) * d + p) * (int)sizeof(double);
 #pragma unroll
       for (int m = 0; m < TS / 8; ++m) {
-        const int r = (tid >> 5) + 8 * m;
-        vi[m] = Xi[r * d + p];
-        vj[m] = Xj[r * d + p];
+        vi[m] = buffer_load_f64(xr, o0, bi + m * os);
+        vj[m] = buffer_load_f64(qr, o0, bj + m * os);
       }
 #pragma unroll
       for (int m = 0; m < TS / 8; ++m) {
@@ -2963,9 +2950,13 @@ __global__ __launch_bounds__(NTHR) void k_pred_cross(DevBatch db) {
     }
   }
   for (int e = tid; e < d + 3; e += NTHR) pw[e] = P[e];
-  if (tid < 128) tab[tid] = g_exp2tab[tid];
+  if (tid < 64) {  // as k_gram
+    const double s2 = P[d], h = g_exp2tab[2 * tid], lo = g_exp2tab[2 * tid + 1];
+    const double th = s2 * h;
+    tab[2 * tid] = th;
+    tab[2 * tid + 1] = fma(s2, h, -th) + s2 * lo;
+  }
   __syncthreads();
-  const double sf2 = pw[d];
   const ExpK ek = g_expk;
   // thread: 4 test points (4mb..) x 4 train points (4rb..)
   const int mb = tid & 15, rb = tid >> 4;
@@ -3012,7 +3003,7 @@ __global__ __launch_bounds__(NTHR) void k_pred_cross(DevBatch db) {
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       const int gm = mtile * TS + 4 * mb + b;
-      const double fv = sf2 * exp_k(-rr[a][b] * 0.5, ek, tab);  // padded points: finite, selected away
+      const double fv = exp_sf(MODE == 1 ? -rr[a][b] : -rr[a][b] * 0.5, ek, tab);  // padded points: finite, selected away
       kv[b] = (inner || (gt < db.N && gm < db.M)) ? fv : 0.0;
       mp[b] = fma(kv[b], alt, mp[b]);
     }
@@ -3022,7 +3013,7 @@ __global__ __launch_bounds__(NTHR) void k_pred_cross(DevBatch db) {
   }
   // the tile's partial means mu_part[ch][m] = sum_{t in tile ch} K*^T[t][m] alpha_t (k_pred_final adds
   // the tiles): the 4 train points of the thread, then the 4 row groups of the wave, then the waves
-  double* mup = tab + 128;  // [4 waves][64 test points]
+  double* mup = sc + DMAX;  // [4 waves][64 test points]
 #pragma unroll
   for (int b = 0; b < 4; ++b) {
     mp[b] += __shfl_xor(mp[b], 16);
@@ -3059,10 +3050,10 @@ __global__ __launch_bounds__(NTHR) void k_pred_final(DevBatch db) {
 // per trajectory, `steps` rounds of  obs = f(q_old, qdot_old);  qdot_cur_g = mu_g(obs) for each of
 // the nc GPs;  (q_old, qdot_old) = (q_cur, qdot_cur);  q_cur += qdot_cur dt.  One workgroup per
 // trajectory runs the whole rollout (the step chain is serial, so it is latency-bound; one launch
-// instead of steps x nc predict calls).  mu_g = sum_j sf2 exp(-r_j/2) alpha_j with r_j summed
-// exactly as k_pred_cross does (training point first, test point second), so a rollout step
-// reproduces gprx_batch_predict's mean up to the exp's rounding (libm's here, k_pred_cross's table
-// exp_k, within 1.3 ulp) and the order of the final sum.  The state updates use
+// instead of steps x nc predict calls).  mu_g = sum_j sf2 exp(-r_j/2) alpha_j with r_j summed as
+// distij does (il2-weighted; k_pred_cross sums coordinates pre-scaled by sqrt(il2/2) instead),
+// so a rollout step reproduces gprx_batch_predict's mean up to rounding: the distance sums', the
+// exp's (libm's here, k_pred_cross's table exp_sf) and the order of the final sum.  The state updates use
 // explicit round-to-nearest mul/add (no fma contraction), as the reference's Julia arithmetic.
 // ============================================================================================
 __device__ __forceinline__ double pick3(const double (&e)[3], int i) {
@@ -3164,7 +3155,7 @@ __global__ __launch_bounds__(NT) void k_rollout(RolloutArgs a) {
 // ---------------------------------------------------------------------------------------------
 static size_t gram_lds(int d) { return (size_t)(2 * d * CS + 2 * DMAX + 4) * sizeof(double); }  // + k_gram's static table
 static size_t lauum_lds(const DevBatch& b) { return lauum_lds_dbl(b.xs, b.nimg) * sizeof(double); }
-static size_t cross_lds(int d) { return (size_t)(2 * d * CS + 2 * DMAX + 4 + 128 + 4 * TS) * sizeof(double); }
+static size_t cross_lds(int d) { return (size_t)(2 * d * CS + 2 * DMAX + 4 + 4 * TS) * sizeof(double); }  // + the static table
 
 static void set_lds_limits() {
   static bool done = false;
