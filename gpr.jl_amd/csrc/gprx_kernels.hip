@@ -891,6 +891,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_rsrc(const void* base, 
 __device__ __forceinline__ double buffer_load_f64(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
   return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
 }
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void buffer_store_f64x2(__amdgpu_buffer_rsrc_t r, int voff, int soff, double x, double y) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_double2(x, y)), r, voff, soff, 0);
+}
 template <int MODE>
 __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
@@ -987,17 +991,18 @@ __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
       }
   }
   double* K = db.K + (size_t)slot * db.mat;
-  double* Kt = K + (size_t)j * TS * db.ld + i * TS;  // the tile (uniform); lane offsets 32-bit
-  const unsigned ldu = (unsigned)db.ld, lof = (unsigned)(4 * cb) * ldu + 4 * rb;
+  // buffer stores over the tile (base uniform): the lane's byte offset in a VGPR, the column step
+  // in an SGPR, no 64-bit address arithmetic per store
+  const __amdgpu_buffer_rsrc_t kr = buffer_rsrc(K + (size_t)j * TS * db.ld + i * TS, 0x7ffffff0);
+  const int ldb = (int)db.ld * (int)sizeof(double), lof = 4 * cb * ldb + 4 * rb * (int)sizeof(double);
   if (i != j && (i + 1) * TS <= db.N) {  // off-diagonal tile inside N x N (block-uniform): no tests
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       double kv[4];
 #pragma unroll
       for (int a = 0; a < 4; ++a) kv[a] = exp_sf(MODE == 1 ? -rr[a][b] : -rr[a][b] * 0.5, ek, tab);
-      double* const Kb = Kt + lof + b * ldu;
-      *(double2*)(Kb) = make_double2(kv[0], kv[1]);
-      *(double2*)(Kb + 2) = make_double2(kv[2], kv[3]);
+      buffer_store_f64x2(kr, lof, b * ldb, kv[0], kv[1]);
+      buffer_store_f64x2(kr, lof + 16, b * ldb, kv[2], kv[3]);
     }
     return;
   }
@@ -1012,9 +1017,8 @@ __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
       const bool pad = gi >= db.N || gj >= db.N;
       kv[a] = (gi == gj) ? (pad ? 1.0 : fv + noise) : (pad ? 0.0 : fv);
     }
-    const size_t off = (size_t)gj * db.ld + i * TS + 4 * rb;
-    *(double2*)(K + off) = make_double2(kv[0], kv[1]);
-    *(double2*)(K + off + 2) = make_double2(kv[2], kv[3]);
+    buffer_store_f64x2(kr, lof, b * ldb, kv[0], kv[1]);
+    buffer_store_f64x2(kr, lof + 16, b * ldb, kv[2], kv[3]);
   }
 }
 
