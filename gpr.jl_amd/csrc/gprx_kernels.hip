@@ -917,13 +917,6 @@ __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
   }
   const double* X = db.X + (size_t)slot * db.Npad * d;
   const double* P = db.params + (size_t)slot * db.pst;
-  // direct mode: coordinates pre-scaled by 1/(sqrt(2) ell_p) = sqrt(il2_p / 2), so that the sums
-  // are r/2, the exponent's magnitude (0.5 il2_p is exact: as accurate as scaling by 1/ell_p)
-  double* sc = pw + DMAX + 4;
-  if (MODE == 1) {
-    for (int e = tid; e < d; e += NTHR) sc[e] = sqrt(0.5 * P[e]);
-    __syncthreads();
-  }
   {  // thread -> (dimension p = tid mod 32 + 32 k, rows tid / 32 + 8 m): no per-element division,
      // 16 loads in flight per thread, coalesced over the 32 dimensions of a point row
     // buffer loads: the lane's byte offset in a VGPR, the row step and tile base in SGPRs, so no
@@ -932,7 +925,6 @@ __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
     const int bi = i * TS * d * (int)sizeof(double), bj = j * TS * d * (int)sizeof(double);
     const int os = 8 * d * (int)sizeof(double);
     for (int p = tid & 31; p < d; p += 32) {
-      const double s = MODE == 1 ? sc[p] : 1.0;
       double vi[TS / 8], vj[TS / 8];
       const int o0 = ((tid >> 5) * d + p) * (int)sizeof(double);
 #pragma unroll
@@ -940,6 +932,10 @@ __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
         vi[m] = buffer_load_f64(xr, o0, bi + m * os);
         vj[m] = buffer_load_f64(xr, o0, bj + m * os);
       }
+      // direct mode: coordinates pre-scaled by 1/(sqrt(2) ell_p) = sqrt(il2_p / 2), so that the
+      // sums are r/2, the exponent's magnitude (0.5 il2_p is exact: as accurate as scaling by
+      // 1/ell_p); each thread scales its own dimension (no staging barrier)
+      const double s = MODE == 1 ? sqrt(0.5 * P[p]) : 1.0;
 #pragma unroll
       for (int m = 0; m < TS / 8; ++m) {
         const int r = (tid >> 5) + 8 * m;
@@ -3157,7 +3153,7 @@ __global__ __launch_bounds__(NT) void k_rollout(RolloutArgs a) {
 // ---------------------------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------------------------
-static size_t gram_lds(int d) { return (size_t)(2 * d * CS + 2 * DMAX + 4) * sizeof(double); }  // + k_gram's static table
+static size_t gram_lds(int d) { return (size_t)(2 * d * CS + DMAX + 4) * sizeof(double); }  // + k_gram's static table
 static size_t lauum_lds(const DevBatch& b) { return lauum_lds_dbl(b.xs, b.nimg) * sizeof(double); }
 static size_t cross_lds(int d) { return (size_t)(2 * d * CS + 2 * DMAX + 4 + 4 * TS) * sizeof(double); }  // + the static table
 
