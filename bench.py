@@ -467,7 +467,7 @@ def main():
     # (gprx.optim.optimize_batch) is timed beside it and must give bit-identical minimisers.
     opt = None
     if not args.no_opt:
-        from gprx.optim import LBFGS, Options, optimize_batch
+        from gprx.optim import LBFGS, Options, compare_optimisers, optimize_batch
 
         def timed(fn):
             barrier()
@@ -483,14 +483,20 @@ def main():
 
         _progress(rank, "optimiser leg")
         o = Options(max_evals=args.opt_evals)
-        (hres, hrounds), t_host = timed(lambda: optimize_batch(batch, T, LBFGS(), o))
-        (res, rounds), t_opt = timed(lambda: batch.optimize(T, LBFGS(), o, refit=True))
-        same = all(np.array_equal(a.minimizer, b.minimizer) and a.minimum == b.minimum for a, b in zip(res, hres))
+        # both legs record their evaluations (theta asked, answer given, per round): a mismatch is
+        # then reported down to the first evaluation where the legs part (compare_optimisers)
+        htrace = []
+        ntr = 4 * args.opt_evals + 8  # rounds to record: more than the budget can use
+        (hres, hrounds), t_host = timed(lambda: optimize_batch(batch, T, LBFGS(), o, trace=htrace))
+        (res, rounds), t_opt = timed(lambda: batch.optimize(T, LBFGS(), o, refit=True, trace_rounds=ntr))
+        cmp = compare_optimisers(res, hres, batch.last_opt_trace, np.stack(htrace) if htrace else None)
+        same = cmp["equal"]
         opt = {"value": round(B * world / t_opt, 3), "unit": "optimised GP fits/s", "max_evals_per_gp": args.opt_evals,
                "optimiser": "device k_lbfgs (+ refit)", "device_rounds": rounds, "seconds": round(t_opt, 3),
                "host_lockstep": {"value": round(B * world / t_host, 3), "seconds": round(t_host, 3),
                                  "device_rounds": hrounds},
                "device_equals_host": bool(same),
+               "device_vs_host": cmp,
                "stopped_by": {k: sum(1 for r in res if r.stopped_by == k) for k in sorted({r.stopped_by for r in res})}}
     cpu = acc = None
     if rank == 0 and not args.no_cpu:

@@ -67,6 +67,8 @@ struct gprx_batch {
   double* h_var = nullptr;
   int* h_status = nullptr;  // pinned, 2B (status, info)
   int* opt_active = nullptr;  // device, B: the optimiser's per-round evaluation mask (DevBatch::active)
+  double* opt_trace = nullptr;  // caller's host buffer for gprx_batch_set_opt_trace (diagnostics)
+  int opt_trace_rounds = 0;
   bool factored = false;
   bool have_train = false;
   bool have_test = false;
@@ -267,7 +269,7 @@ void predict_var(gprx_ctx* c, hipStream_t st, const DevBatch& db) {
   timed(c, st, "pred_var", B * N * N * M, B * 8.0 * (N * N / 2 + N * db.Mpad), [&] { gprx::launch_gemm(db, g, st); });
 }
 void predict_mean_final(gprx_ctx* c, hipStream_t st, const DevBatch& db) {
-  const double N = db.N, M = db.M, B = db.B;
+  const double B = db.B;
   timed(c, st, "pred_final", B * 2.0 * db.nt * db.Mpad, B * 16.0 * db.nt * db.Mpad,
         [&] { gprx::launch_pred_final(db, st); });
 }
@@ -807,6 +809,22 @@ int gprx_batch_optimize(gprx_batch* b, const double* theta0, const gprx_opt_opti
     DevBatch& db;
     ~Unmask() { db.active = nullptr; }
   } um{db};
+  // evaluation trace (gprx_batch_set_opt_trace): per round the evaluated theta and the answer of
+  // every slot, staged in pinned memory (copied under the round's own synchronisation)
+  const int trr = b->opt_trace ? b->opt_trace_rounds : 0;
+  const size_t trs = (size_t)B * (2 * n + 1);  // staged doubles per round: theta(n), out(n + 1)
+  std::vector<int> tr_act((size_t)trr * B, 0);
+  double* h_tr = nullptr;
+  if (trr > 0 && hipHostMalloc((void**)&h_tr, (size_t)trr * trs * sizeof(double)) != hipSuccess) {
+    (void)hipGetLastError();
+    return set_err(c, GPRX_OUT_OF_MEMORY, "gprx_batch_optimize: trace buffer");
+  }
+  struct FreeTr {
+    double* h;
+    ~FreeTr() {
+      if (h) (void)hipHostFree(h);
+    }
+  } ftr{h_tr};
   HIPCHK(c, hipMemcpyAsync(th0d, theta0, (size_t)B * n * sizeof(double), hipMemcpyHostToDevice, c->stream));
   gprx::launch_lbfgs(a, db, 1, c->stream);
   db.active = a.active;
@@ -823,6 +841,13 @@ int gprx_batch_optimize(gprx_batch* b, const double* theta0, const gprx_opt_opti
     int rc = run_eval(b, true, false, true);
     if (rc) return rc;
     collect(c);
+    if (nr < trr) {
+      double* h = h_tr + (size_t)nr * trs;
+      memcpy(&tr_act[(size_t)nr * B], h_act, (size_t)B * sizeof(int));
+      HIPCHK(c, hipMemcpyAsync(h, db.theta, (size_t)B * n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipMemcpyAsync(h + (size_t)B * n, db.out, (size_t)B * (n + 1) * sizeof(double), hipMemcpyDeviceToHost,
+                               c->stream));
+    }
     gprx::launch_lbfgs(a, db, 0, c->stream);
     HIPCHK(c, hipGetLastError());
     ++nr;
@@ -839,6 +864,21 @@ int gprx_batch_optimize(gprx_batch* b, const double* theta0, const gprx_opt_opti
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));
   collect(c);
+  if (trr > 0) {  // [active, theta(n), mll, dmll(n)] per slot and round; NaN beyond the last round
+    const size_t w = 2 * (size_t)n + 2;
+    for (int r = 0; r < trr; ++r)
+      for (int s = 0; s < B; ++s) {
+        double* t = b->opt_trace + ((size_t)r * B + s) * w;
+        if (r >= nr) {
+          for (size_t q = 0; q < w; ++q) t[q] = NAN;
+          continue;
+        }
+        const double* h = h_tr + (size_t)r * trs;
+        t[0] = tr_act[(size_t)r * B + s] ? 1.0 : 0.0;
+        memcpy(t + 1, h + (size_t)s * n, n * sizeof(double));
+        memcpy(t + 1 + n, h + (size_t)B * n + (size_t)s * (n + 1), (n + 1) * sizeof(double));
+      }
+  }
   for (int s = 0; s < B; ++s) {
     const double* r = h_res + (size_t)s * (n + 1);
     if (theta_out) memcpy(theta_out + (size_t)s * n, r, n * sizeof(double));
@@ -861,6 +901,14 @@ int gprx_batch_optimize(gprx_batch* b, const double* theta0, const gprx_opt_opti
     return set_err(c, first, "gprx_batch_optimize: refit at the minimiser of slot " + std::to_string(bad) + ": " +
                                  gprx_status_string(first));
   b->factored = true;
+  return GPRX_OK;
+}
+
+int gprx_batch_set_opt_trace(gprx_batch* b, double* trace, int max_rounds) {
+  if (!b || max_rounds < 0 || (max_rounds > 0 && !trace)) return GPRX_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> g(b->ctx->mu);
+  b->opt_trace = max_rounds > 0 ? trace : nullptr;
+  b->opt_trace_rounds = max_rounds;
   return GPRX_OK;
 }
 

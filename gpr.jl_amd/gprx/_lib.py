@@ -74,6 +74,7 @@ SIGNATURES = {
     "gprx_batch_alpha": (C.c_int, [_vp, _dp]),
     "gprx_opt_defaults": (None, [C.POINTER(OptOptions)]),
     "gprx_batch_optimize": (C.c_int, [_vp, _dp, C.POINTER(OptOptions), _dp, _dp, _ip, _ip, _ip, _ip, _ip]),
+    "gprx_batch_set_opt_trace": (C.c_int, [_vp, _dp, C.c_int]),
     "gprx_gp_create": (C.c_int, [_vp, _dp, C.c_int, C.c_int, _dp, C.POINTER(_vp)]),
     "gprx_gp_destroy": (None, [_vp]),
     "gprx_gp_lml": (C.c_int, [_vp, _dp, _dp]),

@@ -204,14 +204,16 @@ class GPBatch:
             L.check(rc, self.ctx.h)
         return dict(mll=mll, grad=g, mu=mu, var=var, status=st, info=info)
 
-    def optimize(self, theta0, method=None, options=None, refit: bool = True):
+    def optimize(self, theta0, method=None, options=None, refit: bool = True, trace_rounds: int = 0):
         """GaussianProcesses.optimize!(gp, LBFGS(linesearch=BackTracking(order=2)), options) for
         every slot (CPnoise.jl:41), on the device (k_lbfgs: gprx/optim.py's algorithm as a per-slot
         state machine, lock-step over the batch).  method / options: gprx.optim.LBFGS / Options.
         Returns (results, rounds) like gprx.optim.optimize_batch; with refit the batch ends
         factorised at the minimisers (optimize!'s update_target!), so predict() uses them.  A
         minimiser whose refit fails raises (update_target!'s PosDefException / ArgumentError) with
-        the results attached as `err.results`; the batch is then left unfactorised."""
+        the results attached as `err.results`; the batch is then left unfactorised.
+        trace_rounds > 0 records the first rounds' evaluations (gprx_batch_set_opt_trace) in
+        `self.last_opt_trace`: (rounds, B, 2n+2) rows [active, theta(n), mll, dmll(n)], n = d+2."""
         from .optim import Result
 
         o = opt_options(method, options, refit)
@@ -225,8 +227,17 @@ class GPBatch:
         its, fc, gc = (np.empty(B, dtype=np.int32) for _ in range(3))
         stp = np.full(B, -1, dtype=np.int32)  # -1: not written (the call rejected its input)
         rounds = C.c_int(0)
-        rc = L.lib.gprx_batch_optimize(self.h, L.dptr(theta0), C.byref(o), L.dptr(th), L.dptr(fmin), L.iptr(its),
-                                       L.iptr(fc), L.iptr(gc), L.iptr(stp), C.byref(rounds))
+        tr = None
+        if trace_rounds > 0:
+            tr = np.full((int(trace_rounds), B, 2 * n + 2), np.nan)
+            L.check(L.lib.gprx_batch_set_opt_trace(self.h, L.dptr(tr), int(trace_rounds)), self.ctx.h)
+        try:
+            rc = L.lib.gprx_batch_optimize(self.h, L.dptr(theta0), C.byref(o), L.dptr(th), L.dptr(fmin), L.iptr(its),
+                                           L.iptr(fc), L.iptr(gc), L.iptr(stp), C.byref(rounds))
+        finally:
+            if tr is not None:
+                L.lib.gprx_batch_set_opt_trace(self.h, None, 0)
+        self.last_opt_trace = tr[:max(0, min(int(rounds.value), tr.shape[0]))] if tr is not None else None
         if rc not in (L.OK, L.NOT_POSITIVE_DEFINITE, L.INVALID_ARGUMENT) or np.any(stp < 0):
             L.check(rc if rc != L.OK else L.DEVICE_ERROR, self.ctx.h)  # no search ran: no results
         res = [Result(th[s].copy(), float(fmin[s]), int(its[s]), int(fc[s]), int(gc[s]),

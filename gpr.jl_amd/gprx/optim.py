@@ -315,7 +315,8 @@ def optimize(gp, method: LBFGS | None = None, options: Options | None = None) ->
     return res
 
 
-def optimize_batch(batch, theta0, method: LBFGS | None = None, options: Options | None = None):
+def optimize_batch(batch, theta0, method: LBFGS | None = None, options: Options | None = None,
+                   trace: list | None = None):
     """One LBFGS run per slot of a GPBatch (the per-output GPs of CPnoise.jl:37-43 and the trials
     of examples/parallel/core.jl:28), in lock-step: every round answers all pending requests with
     ONE device evaluation of the whole batch (value + gradient for every slot).  Each slot follows
@@ -323,6 +324,8 @@ def optimize_batch(batch, theta0, method: LBFGS | None = None, options: Options 
     the same; only the device calls are shared).  A gradient computed during the line search is
     reused when that point is accepted, within the same round (k_lbfgs does the same).  Failed
     slots answer +Inf as in `optimize`.
+    trace: a list that receives one (B, 2n+2) array per round, rows [active, theta(n), mll,
+    dmll(n)] -- the layout of GPBatch.optimize's `last_opt_trace` (gprx_batch_set_opt_trace).
     Returns (results, rounds)."""
     theta0 = np.asarray(theta0, dtype=np.float64)
     B, npar = theta0.shape
@@ -350,6 +353,10 @@ def optimize_batch(batch, theta0, method: LBFGS | None = None, options: Options 
         if todo:
             rounds += 1
             r = batch.run(th, grad=True, predict=False)
+            if trace is not None:
+                act = np.zeros((B, 1))
+                act[todo] = 1.0
+                trace.append(np.hstack([act, th, np.asarray(r["mll"])[:, None], np.asarray(r["grad"])]))
             for s in todo:
                 x = pending[s][1]
                 if r["status"][s] != 0 or not np.all(np.isfinite(x)):
@@ -373,3 +380,61 @@ def optimize_batch(batch, theta0, method: LBFGS | None = None, options: Options 
                     pending[s] = req
                     break
     return results, rounds
+
+
+def _same_bits(a, b) -> bool:
+    """Bitwise equality of two float arrays (NaN payloads and signed zeros included)."""
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    return a.shape == b.shape and bool(np.array_equal(a.view(np.uint64), b.view(np.uint64)))
+
+
+def compare_optimisers(res_a, res_b, trace_a=None, trace_b=None) -> dict:
+    """Bit-level comparison of two optimiser runs over the same batch (e.g. the device optimiser,
+    GPBatch.optimize, against the host lock-step restatement, optimize_batch).  Minimisers and
+    minima compare by their bits, so equal NaN minima agree.  With both evaluation traces (rows
+    [active, theta(n), mll, dmll(n)] per round) the first differing slot's evaluation sequences
+    are walked in order to name the first evaluation where the two runs part: the same theta
+    answered differently (the evaluation is not reproducible) or a different theta requested (the
+    two optimisers decided differently on equal answers)."""
+    B = len(res_a)
+    bad = [s for s in range(B)
+           if not (_same_bits(res_a[s].minimizer, res_b[s].minimizer)
+                   and _same_bits(np.float64(res_a[s].minimum), np.float64(res_b[s].minimum)))]
+    out = {"equal": not bad, "slots": B, "n_differ": len(bad)}
+    if not bad:
+        return out
+    s = bad[0]
+    a, b = res_a[s], res_b[s]
+    with np.errstate(invalid="ignore"):
+        dth = float(np.max(np.abs(np.asarray(a.minimizer) - np.asarray(b.minimizer))))
+    out.update(first_slot=s, differing_slots=bad[:16], stopped_by=[a.stopped_by, b.stopped_by],
+               f_calls=[a.f_calls, b.f_calls], minimum=[a.minimum, b.minimum], max_abs_dtheta=dth,
+               nonfinite_minimum=[not math.isfinite(a.minimum), not math.isfinite(b.minimum)])
+    if trace_a is None or trace_b is None:
+        return out
+
+    def seq(tr):
+        tr = np.asarray(tr)
+        return [(r, tr[r, s]) for r in range(tr.shape[0]) if tr[r, s, 0] == 1.0]
+
+    sa, sb = seq(trace_a), seq(trace_b)
+    n = (np.asarray(trace_a).shape[2] - 2) // 2
+    first = None
+    for k, ((ra, ea), (rb, eb)) in enumerate(zip(sa, sb)):
+        if not _same_bits(ea[1:1 + n], eb[1:1 + n]):
+            first = dict(index=k, round=[ra, rb], kind="different theta requested",
+                         max_abs_dtheta=float(np.max(np.abs(ea[1:1 + n] - eb[1:1 + n]))))
+            break
+        if not _same_bits(ea[1 + n:], eb[1 + n:]):
+            with np.errstate(invalid="ignore"):
+                dm = abs(float(ea[1 + n]) - float(eb[1 + n]))
+                dg = float(np.max(np.abs(ea[2 + n:] - eb[2 + n:])))
+            first = dict(index=k, round=[ra, rb], kind="same theta answered differently",
+                         mll=[float(ea[1 + n]), float(eb[1 + n])], abs_dmll=dm, max_abs_dgrad=dg)
+            break
+    if first is None and len(sa) != len(sb):
+        first = dict(index=min(len(sa), len(sb)), kind="evaluation counts differ", counts=[len(sa), len(sb)])
+    out["first_eval_diff"] = first
+    out["evaluations"] = [len(sa), len(sb)]
+    return out

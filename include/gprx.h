@@ -188,6 +188,13 @@ void gprx_opt_defaults(gprx_opt_options* opt);
  * and a device / memory error write none of them.                                               */
 int gprx_batch_optimize(gprx_batch* batch, const double* theta0, const gprx_opt_options* opt, double* theta_out,
                         double* minimum, int* iterations, int* f_calls, int* g_calls, int* stopped, int* rounds);
+/* Diagnostics: record the optimiser's evaluations.  With a host buffer of max_rounds * B * (2(d+2)+2)
+ * doubles registered, every later gprx_batch_optimize on this batch writes, for round r < max_rounds
+ * and slot b, at trace[(r*B + b) * (2(d+2)+2)]: [active (1/0: evaluated in this round), theta(d+2)
+ * as evaluated, mll, dmll(d+2) as answered]; rounds past the last are NaN.  The buffer must stay
+ * valid while registered; max_rounds = 0 unregisters it.  (No reference counterpart: it makes the
+ * device optimiser's evaluation sequence comparable with a host restatement's, gprx/optim.py.)  */
+int gprx_batch_set_opt_trace(gprx_batch* batch, double* trace, int max_rounds);
 
 /* ---- single GP: the GPE surface, a batch of one ------------------------------------------- */
 int gprx_gp_create(gprx_ctx* ctx, const double* X, int d, int N, const double* y_minus_mean,

@@ -656,6 +656,44 @@ def test_device_optimize_matches_host_lockstep(gprx, ctx, golden_dir, name, max_
     assert dr == hr
 
 
+def test_device_optimize_bench_shape_bit_identical(gprx, ctx):
+    """The bench's optimiser leg (bench.py, P2noise.jl:41's optimize!): B = 48 slots at N=2048,
+    d=26, a 30-evaluation budget, starts jittered by different amounts so the slots finish at
+    different rounds (masked evaluation rounds at the end).  Device and host minimisers, minima,
+    counts and stop reasons are bit-identical, and so are the two legs' evaluation traces round by
+    round (the same theta asked, the same answer given: gprx_batch_set_opt_trace against
+    optimize_batch's trace)."""
+    from gprx import data
+    from gprx.optim import LBFGS, Options, compare_optimisers, optimize_batch
+
+    B, N = 48, 2048
+    trs = [data.make_trial("P2", N, 0, seed=data.trial_seed("P2", 20 + t)) for t in range(B // 6)]
+    X = np.stack([trs[s // 6]["X"] for s in range(B)])
+    Y = np.stack([trs[s // 6]["Y"][s % 6] for s in range(B)])
+    th0 = data.theta0("P2", 2048)
+    rng = np.random.default_rng(11)
+    amp = np.where(np.arange(B) % 5 == 0, 0.6, 0.05)
+    T = np.stack([th0 + amp[s] * rng.standard_normal(th0.shape[0]) for s in range(B)])
+    b = gprx.GPBatch(B, 26, N, 0, ctx=ctx)
+    b.set_train(X, Y)
+    o = Options(max_evals=30)
+    htr = []
+    host, hr = optimize_batch(b, T, LBFGS(), o, trace=htr)
+    dev, dr = b.optimize(T, LBFGS(), o, refit=True, trace_rounds=160)
+    dtr = b.last_opt_trace
+    htr = np.stack(htr)
+    rep = compare_optimisers(dev, host, dtr, htr)
+    assert rep["equal"], rep
+    _compare_opt(dev, host)
+    assert dr == hr and dtr.shape == htr.shape
+    act = dtr[:, :, 0] == 1.0
+    np.testing.assert_array_equal(act, htr[:, :, 0] == 1.0)
+    np.testing.assert_array_equal(dtr[act].view(np.uint64), htr[act].view(np.uint64))
+    last = [int(np.nonzero(act[:, s])[0].max()) for s in range(B)]
+    assert len(set(last)) > 1, last  # the slots finished at different rounds
+    b.close()
+
+
 def test_device_optimize_ragged_batch_equals_single_slot_runs(gprx, ctx, golden_dir):
     """Slots that stop at different rounds (Optim's own stops, no budget): finished slots are
     masked out of the later rounds' evaluations, and every slot's result is bit-identical to

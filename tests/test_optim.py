@@ -183,3 +183,35 @@ def test_nan_gradient_terminates_early():
     # the loop; f calls = 1 (value_gradient!!) + 1 + 52 trials, g calls = 1 + update_g!
     r = lbfgs_minimize(lambda x: math.inf, lambda x: (math.inf, np.full(2, np.nan)), np.zeros(2))
     assert (r.iterations, r.f_calls, r.g_calls, r.stopped_by, r.converged) == (1, 54, 2, "nan_gradient", False)
+
+
+def test_compare_optimisers_names_the_first_differing_evaluation():
+    """gprx.optim.compare_optimisers (the bench's device_vs_host report): NaN minima compare by
+    their bits, and with both traces the first evaluation where two runs part is named, whether
+    the same theta was answered differently or a different theta was asked."""
+    from gprx.optim import Result, compare_optimisers
+
+    n, B, R = 3, 2, 4
+
+    def res(x, f):
+        return Result(np.array(x, dtype=float), f, 1, 3, 2, False, "max_evals")
+
+    a = [res([1, 2, 3], 1.5), res([0, 0, 0], math.nan)]
+    assert compare_optimisers(a, [res([1, 2, 3], 1.5), res([0, 0, 0], math.nan)])["equal"]
+    tr = np.zeros((R, B, 2 * n + 2))
+    tr[:, :, 0] = 1.0
+    tr[:, :, 1:1 + n] = np.arange(R)[:, None, None] + 0.5
+    tr[:, :, 1 + n] = -np.arange(R)[:, None]
+    tb = tr.copy()
+    tb[2, 1, 1 + n] += 1e-15 * 4  # slot 1's third answer differs in its last bits
+    b = [res([1, 2, 3], 1.5), res([0, 0, 1e-16], math.nan)]
+    rep = compare_optimisers(a, b, tr, tb)
+    assert not rep["equal"] and rep["first_slot"] == 1 and rep["n_differ"] == 1
+    assert rep["first_eval_diff"]["kind"] == "same theta answered differently"
+    assert rep["first_eval_diff"]["index"] == 2 and rep["first_eval_diff"]["round"] == [2, 2]
+    assert rep["nonfinite_minimum"] == [True, True]
+    tc = tr.copy()
+    tc[1, 1, 0] = 0.0  # slot 1 skips round 1 in run c: its second evaluation is round 2's theta
+    rep = compare_optimisers(a, b, tr, tc)
+    assert rep["first_eval_diff"]["kind"] == "different theta requested"
+    assert rep["first_eval_diff"]["round"] == [1, 2]
