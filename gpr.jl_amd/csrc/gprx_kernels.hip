@@ -891,9 +891,15 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_rsrc(const void* base, 
 __device__ __forceinline__ double buffer_load_f64(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
   return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
 }
+// 16-B store at byte offset voff (VGPR).  The SGPR offset field is left 0 on purpose: a MUBUF store
+// with a register soffset is exempt from the compiler's store-data hazard check (no wait state
+// before a VALU overwrites the data VGPRs), and on gfx950 under memory back-pressure (another
+// process on the card) the store then read the NEXT exp's intermediate 1.5*2^52 + n as its data:
+// K elements ~6.76e15, a non-PD pivot in a few evaluations in ten (scratch/concurrency.py).  With
+// soffset 0 the hazard recognizer inserts the wait states.
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void buffer_store_f64x2(__amdgpu_buffer_rsrc_t r, int voff, int soff, double x, double y) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_double2(x, y)), r, voff, soff, 0);
+__device__ __forceinline__ void buffer_store_f64x2(__amdgpu_buffer_rsrc_t r, int voff, double x, double y) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_double2(x, y)), r, voff, 0, 0);
 }
 template <int MODE>
 __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
@@ -987,8 +993,8 @@ __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
       }
   }
   double* K = db.K + (size_t)slot * db.mat;
-  // buffer stores over the tile (base uniform): the lane's byte offset in a VGPR, the column step
-  // in an SGPR, no 64-bit address arithmetic per store
+  // buffer stores over the tile (base uniform): the lane's byte offset in a VGPR (column step
+  // added per store), no 64-bit address arithmetic per store
   const __amdgpu_buffer_rsrc_t kr = buffer_rsrc(K + (size_t)j * TS * db.ld + i * TS, 0x7ffffff0);
   const int ldb = (int)db.ld * (int)sizeof(double), lof = 4 * cb * ldb + 4 * rb * (int)sizeof(double);
   if (i != j && (i + 1) * TS <= db.N) {  // off-diagonal tile inside N x N (block-uniform): no tests
@@ -997,8 +1003,8 @@ __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
       double kv[4];
 #pragma unroll
       for (int a = 0; a < 4; ++a) kv[a] = exp_sf(MODE == 1 ? -rr[a][b] : -rr[a][b] * 0.5, ek, tab);
-      buffer_store_f64x2(kr, lof, b * ldb, kv[0], kv[1]);
-      buffer_store_f64x2(kr, lof + 16, b * ldb, kv[2], kv[3]);
+      buffer_store_f64x2(kr, lof + b * ldb, kv[0], kv[1]);
+      buffer_store_f64x2(kr, lof + b * ldb + 16, kv[2], kv[3]);
     }
     return;
   }
@@ -1013,8 +1019,8 @@ __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
       const bool pad = gi >= db.N || gj >= db.N;
       kv[a] = (gi == gj) ? (pad ? 1.0 : fv + noise) : (pad ? 0.0 : fv);
     }
-    buffer_store_f64x2(kr, lof, b * ldb, kv[0], kv[1]);
-    buffer_store_f64x2(kr, lof + 16, b * ldb, kv[2], kv[3]);
+    buffer_store_f64x2(kr, lof + b * ldb, kv[0], kv[1]);
+    buffer_store_f64x2(kr, lof + b * ldb + 16, kv[2], kv[3]);
   }
 }
 
@@ -1842,9 +1848,11 @@ __global__ __launch_bounds__(NTHR) void k_leaf(DevBatch db, int o, int n, int up
 // of a hung launch.
 // ============================================================================================
 __device__ __forceinline__ int lds_load(const int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+__device__ __forceinline__ void l9_release() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup"); }
+__device__ __forceinline__ void l9_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup"); }
 __device__ __forceinline__ void lds_publish(int* p, int v) {
   // the writer's LDS and global stores are complete before the word changes
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  l9_release();
   if ((threadIdx.x & 63) == 0) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 constexpr int LW_SPIN = 1 << 24;
@@ -1859,7 +1867,7 @@ __device__ __forceinline__ void lds_wait_gt(const int* p, int v, const DevBatch&
     }
     __builtin_amdgcn_s_sleep(1);
   }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  l9_acquire();
 }
 // ---- k_leaf9's diagonal wave: the diagonal routine of diag_tile_fast on one wave.  The 16 x 16
 // factor+inverse is an unscaled elimination (no square root inside the 16-step loop: the columns
@@ -2089,7 +2097,7 @@ __device__ __forceinline__ int l9_wave_of(int e) {
 }
 __device__ __forceinline__ void ctr_barrier(int* ctr, int& gen, int nw, const DevBatch& db, int slot) {
   gen += nw;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  l9_release();
   if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   for (int it = 0; lds_load(ctr) < gen; ++it) {
     if (it > LW_SPIN) {
@@ -2098,7 +2106,7 @@ __device__ __forceinline__ void ctr_barrier(int* ctr, int& gen, int nw, const De
     }
     __builtin_amdgcn_s_sleep(1);
   }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  l9_acquire();
 }
 // acc[a] += sum_k Lx[16a + lk + 4q][k] b(k) for a triangular Lx (lower; LDS image Lx[c * FS + r]):
 // chunk s (k = 4s .. 4s + 3) reaches only the blocks a >= s / 4.  b[s] is lane (lr, lk)'s B operand

@@ -922,3 +922,50 @@ def test_device_optimize_matches_the_independent_oracle(gprx, ctx, golden_dir, n
         assert (dev[s].iterations, dev[s].f_calls, dev[s].g_calls, dev[s].stopped_by, dev[s].converged) == (
             ref["iterations"], ref["f_calls"], ref["g_calls"], ref["stopped_by"], ref["converged"]), s
     b.close()
+
+
+def test_reproducible_beside_another_gpu_process(gprx, ctx):
+    """Evaluations stay bit-identical while another process loads the same GPU (fp64 GEMMs from
+    torch).  Before the k_gram store fix, memory back-pressure let a MUBUF store read its data
+    registers after the next exp had overwritten them: one slot in every few evaluations got K
+    elements ~6.76e15 and a non-PD pivot ("Store-data hazard"; scratch/concurrency.py
+    measured 20% of B=240 evaluations).  Alternating thetas, so a stale or racy value cannot hide
+    behind a repeat of the same inputs."""
+    import subprocess
+    import sys
+    import time
+
+    from gprx import data
+
+    B, N = 96, 2048
+    trs = [data.make_trial("P2", N, 0, seed=data.trial_seed("P2", 40 + t)) for t in range(B // 6)]
+    X = np.stack([trs[s // 6]["X"] for s in range(B)])
+    Y = np.stack([trs[s // 6]["Y"][s % 6] for s in range(B)])
+    th0 = data.theta0("P2", 2048)
+    rng = np.random.default_rng(3)
+    Ta = np.stack([th0 + 0.05 * rng.standard_normal(th0.shape[0]) for _ in range(B)])
+    Tb = Ta + 0.02 * rng.standard_normal(Ta.shape)
+    b = gprx.GPBatch(B, 26, N, 0, ctx=ctx)
+    b.set_train(X, Y)
+    ref = {k: b.run(t, grad=True) for k, t in (("a", Ta), ("b", Tb))}
+    load = ("import time, torch\n"
+            "a = torch.randn(4096, 4096, dtype=torch.float64, device='cuda')\n"
+            "t0 = time.time()\n"
+            "while time.time() - t0 < 25:\n"
+            "    a = torch.tanh(a @ a * 1e-3); torch.cuda.synchronize()\n")
+    p = subprocess.Popen([sys.executable, "-c", load])
+    try:
+        time.sleep(6)  # torch import + first kernels on the card
+        assert p.poll() is None, "load process ended early"
+        n, t0 = 0, time.time()
+        while time.time() - t0 < 12:
+            k = "ab"[n % 2]
+            r = b.run(Ta if k == "a" else Tb, grad=True)
+            n += 1
+            assert np.all(r["status"] == 0), (n, np.nonzero(r["status"])[0], r["info"][r["status"] != 0])
+            np.testing.assert_array_equal(r["mll"], ref[k]["mll"])
+            np.testing.assert_array_equal(r["grad"], ref[k]["grad"])
+        assert n >= 40
+    finally:
+        p.wait(timeout=60)
+        b.close()
