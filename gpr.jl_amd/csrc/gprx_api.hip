@@ -7,6 +7,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <set>
 #include <string>
@@ -382,6 +383,18 @@ int gprx_ctx_create(int device, gprx_ctx** out) {
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return GPRX_DEVICE_ERROR;
+  }
+  {  // kernel attributes of this device, once, before any context on it can launch
+    static std::mutex m;
+    static std::map<int, std::unique_ptr<std::once_flag>> once;
+    std::once_flag* f;
+    {
+      std::lock_guard<std::mutex> g(m);
+      auto& p = once[device];
+      if (!p) p.reset(new std::once_flag());
+      f = p.get();
+    }
+    std::call_once(*f, [] { gprx::set_kernel_attributes(); });
   }
   *out = c;
   return GPRX_OK;

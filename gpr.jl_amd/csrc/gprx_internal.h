@@ -222,6 +222,8 @@ constexpr int LB_LDS_MAX = 160 * 1024;
 size_t lbfgs_lds_bytes(int n, int m);
 
 // kernel launchers (gprx_kernels.hip); every launcher is asynchronous on `s`
+void set_kernel_attributes();  // once per device (gprx_ctx_create), before any launch
+void set_lbfgs_attributes();   // gprx_lbfgs.hip, called by set_kernel_attributes
 void launch_params(const DevBatch& b, hipStream_t s);
 void launch_gram(const DevBatch& b, hipStream_t s);
 void launch_center(const DevBatch& b, hipStream_t s);

@@ -3165,19 +3165,21 @@ static size_t gram_lds(int d) { return (size_t)(2 * d * CS + DMAX + 4) * sizeof(
 static size_t lauum_lds(const DevBatch& b) { return lauum_lds_dbl(b.xs, b.nimg) * sizeof(double); }
 static size_t cross_lds(int d) { return (size_t)(2 * d * CS + 2 * DMAX + 4 + 4 * TS) * sizeof(double); }  // + the static table
 
-static void set_lds_limits() {
-  static bool done = false;
-  if (done) return;
-  done = true;
+// Dynamic-LDS limits above the 64 KB default, for the current device.  Called once per device by
+// gprx_ctx_create (std::call_once per device index) before any launch, so concurrent contexts on
+// other threads never launch a kernel whose attribute is not yet set.
+void set_kernel_attributes() {
   for (const void* f : {(const void*)k_gram<0>, (const void*)k_gram<1>})
     (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)gram_lds(DMAX));
   (void)hipFuncSetAttribute((const void*)k_lauum_grad, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   for (const void* f : {(const void*)k_pred_cross<0>, (const void*)k_pred_cross<1>})
     (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)cross_lds(DMAX));
+  for (const void* f : {(const void*)k_leaf9, (const void*)k_node9})
+    (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)leaf9_lds_bytes());
+  set_lbfgs_attributes();
 }
 
 void launch_gram(const DevBatch& b, hipStream_t s) {
-  set_lds_limits();
   if (b.dist_mode == 0) hipLaunchKernelGGL(k_gram<0>, dim3(grid_blocks(b.B, b.ntl)), dim3(NTHR), gram_lds(b.d), s, b);
   else hipLaunchKernelGGL(k_gram<1>, dim3(grid_blocks(b.B, b.ntl)), dim3(NTHR), gram_lds(b.d), s, b);
 }
@@ -3192,22 +3194,12 @@ void launch_diag(const DevBatch& b, int jt, int upd, hipStream_t s) {
 }
 void launch_leaf(const DevBatch& b, int o, int n, int upd, hipStream_t s) {
   if (n == 4) {
-    static bool attr9 = false;
-    if (!attr9) {
-      attr9 = true;
-      (void)hipFuncSetAttribute((const void*)k_leaf9, hipFuncAttributeMaxDynamicSharedMemorySize, (int)leaf9_lds_bytes());
-    }
     hipLaunchKernelGGL(k_leaf9, dim3(b.B), dim3(2 * NTHR), leaf9_lds_bytes(), s, b, o, upd);
     return;
   }
   hipLaunchKernelGGL(k_leaf, dim3(b.B), dim3(NTHR), 0, s, b, o, n, upd);
 }
 void launch_node8(const DevBatch& b, int o, int upd, hipStream_t s) {
-  static bool attr9 = false;
-  if (!attr9) {
-    attr9 = true;
-    (void)hipFuncSetAttribute((const void*)k_node9, hipFuncAttributeMaxDynamicSharedMemorySize, (int)leaf9_lds_bytes());
-  }
   hipLaunchKernelGGL(k_node9, dim3(b.B), dim3(2 * NTHR), leaf9_lds_bytes(), s, b, o, upd);
 }
 void launch_gemm(const DevBatch& b, const GemmGeom& g, hipStream_t s, const GemmGeom& g2) {
@@ -3230,14 +3222,12 @@ void launch_alpha(const DevBatch& b, hipStream_t s, int phase) {
   hipLaunchKernelGGL(k_alpha, dim3(grid_blocks(b.B, b.nt)), dim3(NTHR), 0, s, b, phase);
 }
 void launch_lauum_grad(const DevBatch& b, hipStream_t s) {
-  set_lds_limits();
   hipLaunchKernelGGL(k_lauum_grad, dim3(grid_blocks(b.B, b.nlj)), dim3(NTHR), lauum_lds(b), s, b);
 }
 void launch_finalize(const DevBatch& b, int want_grad, hipStream_t s) {
   hipLaunchKernelGGL(k_finalize, dim3(b.B), dim3(NTHR), 0, s, b, want_grad);
 }
 void launch_pred_cross(const DevBatch& b, hipStream_t s) {
-  set_lds_limits();
   const dim3 grid(grid_blocks(b.B, b.nt * b.mt));
   if (b.dist_mode == 0) hipLaunchKernelGGL(k_pred_cross<0>, grid, dim3(NTHR), cross_lds(b.d), s, b);
   else hipLaunchKernelGGL(k_pred_cross<1>, grid, dim3(NTHR), cross_lds(b.d), s, b);

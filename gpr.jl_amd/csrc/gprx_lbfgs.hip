@@ -393,12 +393,11 @@ __global__ __launch_bounds__(64) void k_lbfgs_final(LbArgs a, DevBatch db) {
 }
 
 size_t lbfgs_lds_bytes(int n, int m) { return lb_ws_doubles(n, m) * sizeof(double) + LB_NI * sizeof(int); }
+// up to the CU's 160 KB (the default cap is 64 KB); once per device, from set_kernel_attributes
+void set_lbfgs_attributes() {
+  (void)hipFuncSetAttribute((const void*)k_lbfgs, hipFuncAttributeMaxDynamicSharedMemorySize, LB_LDS_MAX);
+}
 void launch_lbfgs(const LbArgs& a, const DevBatch& db, int init, hipStream_t s) {
-  static bool attr = false;
-  if (!attr) {  // up to the CU's 160 KB (the default cap is 64 KB)
-    (void)hipFuncSetAttribute((const void*)k_lbfgs, hipFuncAttributeMaxDynamicSharedMemorySize, LB_LDS_MAX);
-    attr = true;
-  }
   hipLaunchKernelGGL(k_lbfgs, dim3(db.B), dim3(64), lbfgs_lds_bytes(a.n, a.m), s, a, db, init);
 }
 void launch_lbfgs_final(const LbArgs& a, const DevBatch& db, hipStream_t s) {

@@ -969,3 +969,50 @@ def test_reproducible_beside_another_gpu_process(gprx, ctx):
     finally:
         p.wait(timeout=60)
         b.close()
+
+
+def test_first_launches_from_concurrent_contexts_in_a_fresh_process(golden_dir):
+    """Kernel attributes (dynamic LDS above 64 KB: k_leaf9 / k_node9 151 KB, k_lauum_grad, k_lbfgs)
+    are set once per device when a context is created (gprx_ctx_create, std::call_once), not by a
+    process-wide flag at the first launch: four threads of a fresh process each create a context and
+    at once run a B = 32 batch (the fused-leaf path) and its optimiser; every thread gets the serial
+    results."""
+    import subprocess
+    import sys
+
+    script = r'''
+import sys, threading, numpy as np
+sys.path.insert(0, sys.argv[1])
+import gprx
+from gprx import data
+from gprx.optim import LBFGS, Options
+B, N = 32, 256
+trs = [data.make_trial("P2", N, 0, seed=data.trial_seed("P2", t)) for t in range(B // 6 + 1)]
+X = np.stack([trs[s // 6]["X"] for s in range(B)])
+Y = np.stack([trs[s // 6]["Y"][s % 6] for s in range(B)])
+T = np.tile(data.theta0("P2", 256), (B, 1))
+go = threading.Barrier(4)
+out = [None] * 4
+def work(i):
+    go.wait()
+    c = gprx.Context(0)
+    b = gprx.GPBatch(B, 26, N, 0, ctx=c)
+    b.set_train(X, Y)
+    r = b.run(T, grad=True)
+    res, _ = b.optimize(T, LBFGS(), Options(max_evals=6))
+    out[i] = (r["mll"].copy(), r["grad"].copy(), np.stack([q.minimizer for q in res]))
+    b.close(); c.close()
+ts = [threading.Thread(target=work, args=(i,)) for i in range(4)]
+[t.start() for t in ts]; [t.join(120) for t in ts]
+assert all(o is not None for o in out), "a thread failed"
+for o in out[1:]:
+    for a, b in zip(out[0], o):
+        np.testing.assert_array_equal(a, b)
+assert np.all(np.isfinite(out[0][0]))
+print("ok")
+'''
+    import pathlib
+
+    pkg = str(pathlib.Path(__file__).resolve().parents[1] / "gpr.jl_amd")
+    r = subprocess.run([sys.executable, "-c", script, pkg], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
