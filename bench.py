@@ -318,8 +318,6 @@ def _launch_ranks(args) -> int:
     torch.distributed.run child (the driver's own command line), and return its exit code.  Runs
     before this process touches a GPU (device_count() does not initialise one on this image).  Too
     few visible GPUs is an error, not a silent one-rank run; --rehearse lets ranks share devices."""
-    import socket
-
     import torch
 
     ndev = torch.cuda.device_count()
@@ -327,14 +325,11 @@ def _launch_ranks(args) -> int:
         print(f"bench: --gpus {args.gpus} needs {args.gpus} visible GPUs, this host has {ndev} "
               f"(--rehearse runs the ranks on shared devices, for a rehearsal only)", file=sys.stderr)
         return 2
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
-           "--master-addr", "127.0.0.1", "--master-port", str(port), str(pathlib.Path(__file__).resolve()),
-           *sys.argv[1:]]
-    _progress(0, f"launching {args.gpus} ranks: {' '.join(cmd[1:6])} ...")
+    # the command line of gprx.shard.launch_cmd (c10d rendezvous on a free port of 127.0.0.1),
+    # written out here so that this parent never imports the library
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", str(pathlib.Path(__file__).resolve()), *sys.argv[1:]]
+    _progress(0, f"launching {args.gpus} ranks: {' '.join(cmd[1:8])} ...")
     import subprocess
 
     return subprocess.run(cmd).returncode

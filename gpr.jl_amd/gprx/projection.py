@@ -125,14 +125,14 @@ def predictdynamics(mech: str, groups, start, steps: int, vw_indices, regularize
 
 
 def _default_ctx():
-    """The context of this process's current device (a rank bound to GPU LOCAL_RANK by
-    shard.init_ranks gets its own device's context)."""
+    """The context of this rank's device: GPU LOCAL_RANK (mod the visible devices, as
+    shard.init_ranks binds a rank; 0 without a launcher).  Read from the environment, not from
+    torch, so that a library call without a ctx neither initialises torch's HIP runtime nor picks a
+    device other than the one the rank's own contexts use."""
+    import os
+
     from .batch import default_context
 
-    try:
-        import torch
-
-        dev = torch.cuda.current_device() if torch.cuda.is_available() else 0
-    except ImportError:
-        dev = 0
+    n = int(L.lib.gprx_device_count())
+    dev = int(os.environ.get("LOCAL_RANK", "0") or 0) % max(1, n)
     return default_context(dev)

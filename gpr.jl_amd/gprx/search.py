@@ -209,7 +209,7 @@ def main(argv=None):
         if "WORLD_SIZE" not in os.environ and a.gpus > 1:  # parent: no GPU call has been made
             import sys
 
-            raise SystemExit(shard.launch_ranks(os.path.abspath(sys.argv[0]), a.gpus, a.rehearse,
+            raise SystemExit(shard.launch_ranks(shard.entry_script("search"), a.gpus, a.rehearse,
                                                 sys.argv[1:] if argv is None else list(argv), "search"))
         shard.check_world(a.gpus, "search")
     world = shard.init_ranks(a.rehearse)

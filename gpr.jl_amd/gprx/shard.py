@@ -53,14 +53,31 @@ def init_ranks(rehearse: bool = False) -> int:
     return world
 
 
+def entry_script(name: str) -> str:
+    """The repo-root wrapper (sweep.py, search.py) that a self-launch starts on every rank, whatever
+    way this process was started (`python sweep.py`, `python -m gprx.sweep`, main() from code):
+    sys.argv[0] names the package module under -m, which cannot run as a plain script."""
+    import pathlib
+
+    return str(pathlib.Path(__file__).resolve().parents[2] / f"{name}.py")
+
+
+def launch_cmd(script: str, gpus: int, argv: list[str]) -> list[str]:
+    """torch.distributed.run for one node, N ranks: a c10d rendezvous that binds its own free port
+    on 127.0.0.1 (--standalone; no probe-then-reuse race on a port number)."""
+    import sys
+
+    return [sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1", "--nnodes=1",
+            f"--nproc-per-node={gpus}", script, *argv]
+
+
 def launch_ranks(script: str, gpus: int, rehearse: bool, argv: list[str], tag: str = "gprx") -> int:
     """`<script> --gpus N` (N > 1) started without a launcher: start N ranks, one per GPU, as a
-    torch.distributed.run child running the same script and arguments (the driver's own command
-    line), and return its exit code.  Call before this process touches a GPU (device_count() does
-    not initialise one on this image).  Fewer visible GPUs than N is an error (exit 2), not a silent
-    one-rank run; `rehearse` lets ranks share devices.  bench.py, sweep.py and search.py all start
-    their ranks through this."""
-    import socket
+    torch.distributed.run child running `script` with `argv`, and return its exit code.  Call
+    before this process touches a GPU (device_count() does not initialise one on this image).
+    Fewer visible GPUs than N is an error (exit 2), not a silent one-rank run; `rehearse` lets
+    ranks share devices.  sweep.py and search.py start their ranks through this; bench.py keeps a
+    copy of it (_launch_ranks, same command line) so that its parent never imports the library."""
     import subprocess
     import sys
 
@@ -71,13 +88,8 @@ def launch_ranks(script: str, gpus: int, rehearse: bool, argv: list[str], tag: s
         print(f"{tag}: --gpus {gpus} needs {gpus} visible GPUs, this host has {ndev} "
               f"(--rehearse runs the ranks on shared devices, for a rehearsal only)", file=sys.stderr)
         return 2
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
-           "--master-addr", "127.0.0.1", "--master-port", str(port), script, *argv]
-    print(f"{tag}: launching {gpus} ranks: {' '.join(cmd[1:6])} ...", file=sys.stderr, flush=True)
+    cmd = launch_cmd(script, gpus, argv)
+    print(f"{tag}: launching {gpus} ranks: {' '.join(cmd[1:8])} ...", file=sys.stderr, flush=True)
     return subprocess.run(cmd).returncode
 
 

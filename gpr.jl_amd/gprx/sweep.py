@@ -321,7 +321,7 @@ def main(argv=None):
         if "WORLD_SIZE" not in os.environ and a.gpus > 1:  # parent: no GPU call has been made
             import sys
 
-            raise SystemExit(shard.launch_ranks(os.path.abspath(sys.argv[0]), a.gpus, a.rehearse,
+            raise SystemExit(shard.launch_ranks(shard.entry_script("sweep"), a.gpus, a.rehearse,
                                                 sys.argv[1:] if argv is None else list(argv), "sweep"))
         shard.check_world(a.gpus, "sweep")
     world = shard.init_ranks(a.rehearse)

@@ -113,3 +113,31 @@ def test_drivers_refuse_more_ranks_than_gpus(script):
     p = subprocess.run([sys.executable, os.path.join(REPO, script), "--gpus", "2", "--trials", "1"], capture_output=True,
                        text=True, timeout=300, env=dict(env, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0"))
     assert p.returncode == 2 and "WORLD_SIZE=1" in p.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("entry", ["module", "script"])
+def test_sweep_self_launch_two_ranks_equals_one_rank(tmp_path, entry):
+    """The launch path itself, not only its refusals: `python -m gprx.sweep --gpus 2 --rehearse`
+    (and `python sweep.py ...`) starts two ranks through shard.launch_ranks (the repo-root wrapper
+    on every rank, a c10d rendezvous on a free 127.0.0.1 port), the ranks share the one card over a
+    gloo control plane, and the gathered checkpoint equals the one-rank run's."""
+    args = ["--mechs", "P2", "--sizes", "8", "--variants", "min,max", "--trials", "4", "--testsamples", "3",
+            "--simsteps", "3", "--max-evals", "6"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    one, two = tmp_path / "one.json", tmp_path / "two.json"
+    p = subprocess.run([sys.executable, os.path.join(REPO, "sweep.py"), *args, "--out", str(one)], capture_output=True,
+                       text=True, timeout=300, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    if entry == "module":
+        cmd, cwd = [sys.executable, "-m", "gprx.sweep"], os.path.join(REPO, "gpr.jl_amd")
+    else:
+        cmd, cwd = [sys.executable, os.path.join(REPO, "sweep.py")], REPO
+    p = subprocess.run([*cmd, *args, "--gpus", "2", "--rehearse", "--out", str(two)], capture_output=True, text=True,
+                       timeout=300, env=env, cwd=cwd)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
+    import json
+
+    a, b = json.loads(one.read_text()), json.loads(two.read_text())
+    assert b["world"] == 2 and a["world"] == 1
+    assert a["results"] == b["results"]
