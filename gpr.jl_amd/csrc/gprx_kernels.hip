@@ -364,21 +364,40 @@ __device__ __forceinline__ void mma_64x32_s1(d4 (&acc)[WM][WN], const double* __
 // TF/s at K = 1024 / 512 / 256, against 64.5 / 67.4 / 63.0 for depth-16 stages without the
 // barriers (and 60.2 / 57.4 / 52.7 for depth 16 with them: 25 spills).
 // ---------------------------------------------------------------------------------------------
+// Buffer resource over [base, base + bytes) (gfx9 word 3: raw, bounds-checked) and a 64-bit load
+// at byte offset voff (VGPR) + soff (SGPR): out-of-range reads return 0.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_rsrc(const void* base, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes, 0x00020000);
+}
+__device__ __forceinline__ double buffer_load_f64(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
+}
+// 16-B store at byte offset voff (VGPR).  The SGPR offset field is left 0 on purpose: a MUBUF store
+// with a register soffset is exempt from the compiler's store-data hazard check (no wait state
+// before a VALU overwrites the data VGPRs), and on gfx950 under memory back-pressure (another
+// process on the card) the store then read the NEXT exp's intermediate 1.5*2^52 + n as its data:
+// K elements ~6.76e15, a non-PD pivot in a few evaluations in ten (scratch/concurrency.py).  With
+// soffset 0 the hazard recognizer inserts the wait states.
+// 8-B store at byte offset voff (VGPR) + soff (SGPR): 64-bit data, no store-data hazard (a VALU
+// overwrite of >64-bit store data needs wait states the compiler skips for a register soffset;
+// see buffer_store_f64x2)
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void buffer_store_f64(__amdgpu_buffer_rsrc_t r, int voff, int soff, double x) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, x), r, voff, soff, 0);
+}
+// -x by the sign bit (exact, as a multiply by -1; an integer VALU op)
+__device__ __forceinline__ double neg_f64(double x) {
+  return __builtin_bit_cast(double, __builtin_bit_cast(unsigned long long, x) ^ 0x8000000000000000ull);
+}
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void buffer_store_f64x2(__amdgpu_buffer_rsrc_t r, int voff, double x, double y) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_double2(x, y)), r, voff, 0, 0);
+}
 constexpr int QM = 4, QN = 4, Q4SD = 2;
 struct Frag4 {
   double a[Q4SD][QM], b[Q4SD][QN];
 };
 // NB < QN: only the first NB 16-column blocks of B (the prediction's last, partly padded test tile)
-template <int NB = QN>
-__device__ __forceinline__ void frag4_load(Frag4& f, const double* pa, const double* pb, ptrdiff_t sa, ptrdiff_t sb) {
-#pragma unroll
-  for (int s = 0; s < Q4SD; ++s) {
-#pragma unroll
-    for (int a = 0; a < QM; ++a) f.a[s][a] = pa[s * sa + 16 * a];
-#pragma unroll
-    for (int b = 0; b < NB; ++b) f.b[s][b] = pb[s * sb + 16 * b];
-  }
-}
 template <int NB = QN>
 __device__ __forceinline__ void frag4_mma(d4 (&acc)[QM][QN], const Frag4& f) {
 #pragma unroll
@@ -387,38 +406,6 @@ __device__ __forceinline__ void frag4_mma(d4 (&acc)[QM][QN], const Frag4& f) {
     for (int a = 0; a < QM; ++a)
 #pragma unroll
       for (int b = 0; b < NB; ++b) acc[a][b] = mfma(f.b[s][b], f.a[s][a], acc[a][b]);
-}
-template <int NB = QN>
-__device__ __forceinline__ void mma_64x64(d4 (&acc)[QM][QN], const double* __restrict__ A, size_t lda,
-                                          const double* __restrict__ B, size_t ldb, int K) {
-  const int nst = __builtin_amdgcn_readfirstlane(K / (4 * Q4SD));  // even: K is whole 64-tiles
-  if (nst <= 0) return;
-  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
-  const double* pa = A + lr + (ptrdiff_t)lk * (ptrdiff_t)lda;
-  const double* pb = B + lr + (ptrdiff_t)lk * (ptrdiff_t)ldb;
-  const ptrdiff_t sa = 4 * (ptrdiff_t)lda, sb = 4 * (ptrdiff_t)ldb;
-  Frag4 f0, f1;
-  frag4_load<NB>(f0, pa, pb, sa, sb);
-  for (int it = 0; it < nst; it += 2) {
-    __builtin_amdgcn_sched_barrier(0);
-    frag4_load<NB>(f1, pa + (ptrdiff_t)(it + 1) * Q4SD * sa, pb + (ptrdiff_t)(it + 1) * Q4SD * sb, sa, sb);
-    frag4_mma<NB>(acc, f0);
-#pragma unroll
-    for (int g = 0; g < Q4SD * (QM + NB); ++g) {
-      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // one VMEM read
-      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // two MFMAs
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    const int n2 = (it + 2 < nst) ? it + 2 : nst - 1;
-    frag4_load<NB>(f0, pa + (ptrdiff_t)n2 * Q4SD * sa, pb + (ptrdiff_t)n2 * Q4SD * sb, sa, sb);
-    frag4_mma<NB>(acc, f1);
-#pragma unroll
-    for (int g = 0; g < Q4SD * (QM + NB); ++g) {
-      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-  }
 }
 // mma_64x64 with triangular operand tiles and lower-only outputs skipped at 16 x 16-block
 // granularity.  A 64-K tile of the K loop is 8 stages (k = 8s..8s+7), i.e. 4 loop trips of 2 stages.
@@ -435,25 +422,51 @@ __device__ __forceinline__ void mma_64x64(d4 (&acc)[QM][QN], const double* __res
 // bit-identical to the full core's.  Shared panels (B = A) load the fragments once.
 enum CoreMode { PLAIN = 0, TRI_A_FIRST, TRI_AB_FIRST, LOWER_SAME, TRI_A_LAST, TRI_B_LAST, REV_A, REV_B };
 // Operand addressing: element (row, k) at base[row + k ld]; lane (lr, lk) of sub-step s of stage st
-// reads k = 8 st + 4 s + lk of rows 16 a + lr (a 16-row block reads 128 contiguous bytes).
+// reads k = 8 st + 4 s + lk of rows 16 a + lr (a 16-row block reads 128 contiguous bytes).  Round 5:
+// buffer loads, the lane's byte offset in a VGPR (fixed), the stage and sub-step offsets in SGPRs
+// and the row block in the instruction's offset field, so the K loop has no VALU address
+// arithmetic (64-bit global addresses needed a v_lshl_add_u64 per address per stage, and every
+// VALU instruction takes issue cycles from the other wave's MFMAs on gfx950: the core pattern on an
+// L2-resident panel ran at 76.4 TF/s with global loads and 77.6 with buffer loads,
+// scratch/mfma_pattern.hip, profiles/r05_mfma_valu_pattern.txt).
 struct CorePtr {
+  __amdgpu_buffer_rsrc_t r;  // over the operand from its tile origin
+  int vo;                    // this lane's byte offset: row lr, column lk
+  int o;                     // byte offset of stage 0, sub-step 0 (wave-uniform)
+  int st, sub;               // stage / sub-step strides in bytes (negative: a backward walk)
+};
+__device__ __forceinline__ CorePtr core_ptr(const double* X, size_t ld) {
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  const int L = (int)ld * (int)sizeof(double);
+  return CorePtr{buffer_rsrc(X, 0x7ffffff0), lr * (int)sizeof(double) + lk * L, 0, 8 * L, 4 * L};
+}
+__device__ __forceinline__ CorePtr core_rev(CorePtr c, int nst) {  // stages and sub-steps backward
+  c.o += (nst - 1) * c.st + c.sub;
+  c.st = -c.st;
+  c.sub = -c.sub;
+  return c;
+}
+// The same walk through 64-bit global addresses (the round-4 form): k_node9 keeps it, since its
+// GEMM phases sit beside the fused leaf's state and the buffer form's SGPR resources pushed that
+// kernel from 8 to 58 spilled VGPRs.
+struct CorePtrG {
   const double* p;  // this lane's address of stage 0, sub-step 0, row block 0
   ptrdiff_t st;     // stage stride
   ptrdiff_t sub;    // sub-step stride
 };
-__device__ __forceinline__ CorePtr core_ptr(const double* X, size_t ld) {
+__device__ __forceinline__ CorePtrG core_ptr_g(const double* X, size_t ld) {
   const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
   const ptrdiff_t L = (ptrdiff_t)ld;
-  return CorePtr{X + lr + lk * L, 8 * L, 4 * L};
+  return CorePtrG{X + lr + lk * L, 8 * L, 4 * L};
 }
-__device__ __forceinline__ CorePtr core_rev(CorePtr c, int nst) {  // stages and sub-steps backward
+__device__ __forceinline__ CorePtrG core_rev(CorePtrG c, int nst) {
   c.p += (ptrdiff_t)(nst - 1) * c.st + c.sub;
   c.st = -c.st;
   c.sub = -c.sub;
   return c;
 }
 template <int A0, int A1, int B0, int B1, bool SAME>
-__device__ __forceinline__ void frag4_load_r(Frag4& f, const CorePtr& A, const CorePtr& B, int st) {
+__device__ __forceinline__ void frag4_load_r(Frag4& f, const CorePtrG& A, const CorePtrG& B, int st) {
   constexpr int L0 = SAME ? (A0 < B0 ? A0 : B0) : A0, L1 = SAME ? (A1 > B1 ? A1 : B1) : A1;
   const double* pa = A.p + (ptrdiff_t)st * A.st;
   const double* pb = B.p + (ptrdiff_t)st * B.st;
@@ -464,6 +477,25 @@ __device__ __forceinline__ void frag4_load_r(Frag4& f, const CorePtr& A, const C
     if constexpr (!SAME) {
 #pragma unroll
       for (int b = B0; b < B1; ++b) f.b[s][b] = pb[s * B.sub + 16 * b];
+    }
+  }
+}
+template <bool BUF>
+__device__ __forceinline__ auto core_addr(const double* X, size_t ld) {
+  if constexpr (BUF) return core_ptr(X, ld);
+  else return core_ptr_g(X, ld);
+}
+template <int A0, int A1, int B0, int B1, bool SAME>
+__device__ __forceinline__ void frag4_load_r(Frag4& f, const CorePtr& A, const CorePtr& B, int st) {
+  constexpr int L0 = SAME ? (A0 < B0 ? A0 : B0) : A0, L1 = SAME ? (A1 > B1 ? A1 : B1) : A1;
+  const int oa = A.o + st * A.st, ob = B.o + st * B.st;
+#pragma unroll
+  for (int s = 0; s < Q4SD; ++s) {
+#pragma unroll
+    for (int a = L0; a < L1; ++a) f.a[s][a] = buffer_load_f64(A.r, A.vo + 128 * a, oa + s * A.sub);
+    if constexpr (!SAME) {
+#pragma unroll
+      for (int b = B0; b < B1; ++b) f.b[s][b] = buffer_load_f64(B.r, B.vo + 128 * b, ob + s * B.sub);
     }
   }
 }
@@ -479,6 +511,37 @@ __device__ __forceinline__ void frag4_mma_r(d4 (&acc)[QM][QN], const Frag4& f) {
         acc[a][b] = mfma(SAME ? f.a[s][b] : f.b[s][b], f.a[s][a], acc[a][b]);
       }
 }
+// the prediction variance's core (k_gemm_pv): NB < QN: only the first NB 16-column blocks of B
+// (the last, partly padded test tile); operands through CorePtr like the triangular cores
+template <int NB = QN>
+__device__ __forceinline__ void mma_64x64(d4 (&acc)[QM][QN], const double* __restrict__ A, size_t lda,
+                                          const double* __restrict__ B, size_t ldb, int K) {
+  const int nst = __builtin_amdgcn_readfirstlane(K / (4 * Q4SD));  // even: K is whole 64-tiles
+  if (nst <= 0) return;
+  const CorePtr pa = core_ptr(A, lda), pb = core_ptr(B, ldb);
+  Frag4 f0, f1;
+  frag4_load_r<0, QM, 0, NB, false>(f0, pa, pb, 0);
+  for (int it = 0; it < nst; it += 2) {
+    __builtin_amdgcn_sched_barrier(0);
+    frag4_load_r<0, QM, 0, NB, false>(f1, pa, pb, it + 1);
+    frag4_mma<NB>(acc, f0);
+#pragma unroll
+    for (int g = 0; g < Q4SD * (QM + NB); ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // one VMEM read
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // two MFMAs
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const int n2 = (it + 2 < nst) ? it + 2 : nst - 1;
+    frag4_load_r<0, QM, 0, NB, false>(f0, pa, pb, n2);
+    frag4_mma<NB>(acc, f1);
+#pragma unroll
+    for (int g = 0; g < Q4SD * (QM + NB); ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
 // masks of trip T (0..3) of the triangular tile; T = 4: the dense trips
 template <int MODE, int T>
 struct TripMask {
@@ -489,8 +552,8 @@ struct TripMask {
   static constexpr int b0 = (!dense && MODE == TRI_B_LAST) ? T : (!dense && MODE == REV_B) ? 3 - T : 0;
   static constexpr int b1 = (!dense && MODE == TRI_AB_FIRST) ? T + 1 : QN;
 };
-template <int MODE, int T>
-__device__ __forceinline__ void core_load(Frag4& f, const CorePtr& A, const CorePtr& B, int st) {
+template <int MODE, int T, class CP>
+__device__ __forceinline__ void core_load(Frag4& f, const CP& A, const CP& B, int st) {
   constexpr bool same = MODE == TRI_AB_FIRST || MODE == LOWER_SAME;
   using M = TripMask<MODE, T>;
   frag4_load_r<M::a0, M::a1, M::b0, M::b1, same>(f, A, B, st);
@@ -577,12 +640,12 @@ __device__ __forceinline__ void mma_64x64_m(d4 (&acc)[QM][QN], const double* __r
 // loop: TT walks K forward from its upper-triangular first tile (Mt[ti,ti]); TRSM and LINV21 walk
 // K backward from their lower-triangular last tile (Linv[tj,tj], Linv[ti,ti]: reversed trip T
 // needs the row / column blocks >= 3 - T).  tri: this wave's op is PM's.
-template <int PM>
+template <int PM, bool BUF = true>
 __device__ __forceinline__ void mma_64x64_pm(d4 (&acc)[QM][QN], const double* __restrict__ A, size_t lda,
                                              const double* __restrict__ B, size_t ldb, int K, bool tri) {
   const int nst = __builtin_amdgcn_readfirstlane(K / (4 * Q4SD));
   if (nst <= 0) return;
-  CorePtr pa = core_ptr(A, lda), pb = core_ptr(B, ldb);
+  auto pa = core_addr<BUF>(A, lda), pb = core_addr<BUF>(B, ldb);
   Frag4 f0, f1;
   int it = 0;
   if (tri) {
@@ -883,24 +946,6 @@ __device__ __forceinline__ void acc_zero(d4 (&acc)[WM][WN]) {
 // a point in one bank (26-way conflicts on each ds_write_b64); 66 spreads them over the banks and
 // keeps the 16-B alignment of the inner loop's ds_read_b128.
 constexpr int CS = TS + 2;
-// Buffer resource over [base, base + bytes) (gfx9 word 3: raw, bounds-checked) and a 64-bit load
-// at byte offset voff (VGPR) + soff (SGPR): out-of-range reads return 0.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_rsrc(const void* base, int bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes, 0x00020000);
-}
-__device__ __forceinline__ double buffer_load_f64(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
-  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
-}
-// 16-B store at byte offset voff (VGPR).  The SGPR offset field is left 0 on purpose: a MUBUF store
-// with a register soffset is exempt from the compiler's store-data hazard check (no wait state
-// before a VALU overwrites the data VGPRs), and on gfx950 under memory back-pressure (another
-// process on the card) the store then read the NEXT exp's intermediate 1.5*2^52 + n as its data:
-// K elements ~6.76e15, a non-PD pivot in a few evaluations in ten (scratch/concurrency.py).  With
-// soffset 0 the hazard recognizer inserts the wait states.
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void buffer_store_f64x2(__amdgpu_buffer_rsrc_t r, int voff, double x, double y) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_double2(x, y)), r, voff, 0, 0);
-}
 template <int MODE>
 __global__ __launch_bounds__(NTHR) void k_gram(DevBatch db) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
@@ -1254,7 +1299,7 @@ __device__ __forceinline__ void diag_store(const DevBatch& db, int slot, int jt,
 // ============================================================================================
 // One 64 x 64 output tile (ti, tj) of a GemmOp on one wave.
 constexpr int TT_S = TS + 2;  // row stride of k_gemm's per-wave transpose buffer (LINV21's Mt store)
-template <bool PV, int PM = PLAIN>
+template <bool PV, int PM = PLAIN, bool BUF = true>
 __device__ __forceinline__ void gemm_tile(const DevBatch& db, const GemmGeom& g, int slot, int ti, int tj, int pass = 0) {
   GTS(g, pass, 0);
   const int op = PV ? (int)OP_PREDVAR : g.op;
@@ -1276,15 +1321,20 @@ __device__ __forceinline__ void gemm_tile(const DevBatch& db, const GemmGeom& g,
       break;
   }
   const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  // the output tile's addressing (the SYRK's C and every op's stores): buffer ops over the tile,
+  // the lane's byte offset per q in a VGPR, the 16-column block b in an SGPR, the row block a in the
+  // offset field: no per-element 64-bit address arithmetic
+  const int Lb = (int)ld * (int)sizeof(double);
+  const int vl = lk * Lb + lr * (int)sizeof(double);  // + 4 q Lb (formed where used: not live across the K loop)
   d4 acc[QM][QN];
   if (op == OP_SYRK) {  // acc = -C, loaded before the K loop so its latency overlaps the first stage
-    const double* Cs = (g.upd ? db.S : db.K) + so + (size_t)(tj * TS) * ld + ti * TS;
+    const __amdgpu_buffer_rsrc_t cr = buffer_rsrc((g.upd ? db.S : db.K) + so + (size_t)(tj * TS) * ld + ti * TS, 0x7ffffff0);
 #pragma unroll
     for (int a = 0; a < QM; ++a)
 #pragma unroll
       for (int b = 0; b < QN; ++b)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) acc[a][b][q] = -Cs[(size_t)(16 * b + lk + 4 * q) * ld + 16 * a + lr];
+        for (int q = 0; q < 4; ++q) acc[a][b][q] = neg_f64(buffer_load_f64(cr, vl + 128 * a, (16 * b + 4 * q) * Lb));
   } else {
     acc4_zero(acc);
   }
@@ -1305,7 +1355,7 @@ __device__ __forceinline__ void gemm_tile(const DevBatch& db, const GemmGeom& g,
     const int Kn = (ke - kb) * TS;
     const bool tri = (PM == TRI_A_FIRST && op == OP_TT) || (PM == REV_A && op == OP_LINV21) || (PM == REV_B && op == OP_TRSM);
     GTS(g, pass, 1);
-    mma_64x64_pm<PM>(acc, Ak, ld, Bk, ldb, Kn, tri);
+    mma_64x64_pm<PM, BUF>(acc, Ak, ld, Bk, ldb, Kn, tri);
     GTS(g, pass, 2);
 #ifdef GPRX_STAMPS
     if ((op == OP_SYRK || op == OP_TT) && g.n == db.nt) {
@@ -1331,24 +1381,30 @@ __device__ __forceinline__ void gemm_tile(const DevBatch& db, const GemmGeom& g,
     return;
   }
   double* Cm;
-  double sgn = 1.0;
   switch (op) {
     case OP_TRSM: Cm = db.Lw + so; break;
     case OP_SYRK: Cm = db.S + so; break;
     case OP_TT: Cm = db.Lw + so; break;
-    default: Cm = db.Linv + so; sgn = -1.0; break;
+    default: Cm = db.Linv + so; break;
   }
-  double* Ct = Cm + (size_t)(tj * TS) * ld + ti * TS;
+  // SYRK: C - L L^T = -acc; LINV21: L^-1_21 = -acc.  The sign flips the sign bit (an integer op:
+  // an fp64 multiply by -1 takes issue cycles from the MFMA pipe of the SIMD's other wave)
+  if (op == OP_SYRK || op == OP_LINV21) {  // wave-uniform
+#pragma unroll
+    for (int a = 0; a < QM; ++a)
+#pragma unroll
+      for (int b = 0; b < QN; ++b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[a][b][q] = neg_f64(acc[a][b][q]);
+  }
+  const __amdgpu_buffer_rsrc_t crw = buffer_rsrc(Cm + (size_t)(tj * TS) * ld + ti * TS, 0x7ffffff0);
 #pragma unroll
   for (int a = 0; a < QM; ++a)
 #pragma unroll
     for (int b = 0; b < QN; ++b)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        double* p = Ct + (size_t)(16 * b + lk + 4 * q) * ld + 16 * a + lr;
-        *p = (op == OP_SYRK ? -1.0 : sgn) * acc[a][b][q];  // SYRK: C - L L^T = -acc
-      }
-  if (op == OP_LINV21) zp_acc4(db, slot, ti, tj, acc, -1.0);
+      for (int q = 0; q < 4; ++q) buffer_store_f64(crw, vl + 128 * a, (16 * b + 4 * q) * Lb, acc[a][b][q]);
+  if (op == OP_LINV21) zp_acc4(db, slot, ti, tj, acc, 1.0);
   if (op != OP_LINV21) GTS(g, pass, 3);
   if (op == OP_LINV21) {  // Mt[tj, ti] = Linv[ti, tj]^T, transposed through LDS 16 rows at a time
     // so that every store instruction writes one contiguous 512-B column segment of Mt
@@ -1362,7 +1418,7 @@ __device__ __forceinline__ void gemm_tile(const DevBatch& db, const GemmGeom& g,
 #pragma unroll
       for (int b = 0; b < QN; ++b)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) tb[lr * TT_S + 16 * b + lk + 4 * q] = -acc[a][b][q];
+        for (int q = 0; q < 4; ++q) tb[lr * TT_S + 16 * b + lk + 4 * q] = acc[a][b][q];
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
       for (int r = 0; r < 16; ++r) Mtt[(size_t)(16 * a + r) * ld + l] = tb[r * TT_S + l];
@@ -1390,7 +1446,7 @@ __device__ __forceinline__ int gemm_units(const DevBatch& db, const GemmGeom& g1
   return T1 + ((plan || g2.op == OP_NONE) ? 0 : op_units(g2, db.nt, db.mt));
 }
 // unit u of a slot on the four waves w = 0..3 that share it
-template <bool PV, int PM = PLAIN>
+template <bool PV, int PM = PLAIN, bool BUF = true>
 __device__ __forceinline__ void gemm_unit(const DevBatch& db, const GemmGeom& g1, const GemmGeom& g2, int slot, int u, int w,
                                           int T1) {
   int r0, c0, R, C, r02, c02, R2, C2;
@@ -1459,7 +1515,7 @@ __device__ __forceinline__ void gemm_unit(const DevBatch& db, const GemmGeom& g1
       tj = c0 + uc + wc;
     }
     // wave-uniform tile indices in SGPRs (the 64 x 64 core needs every VGPR)
-    gemm_tile<PV, PM>(db, sel ? g2 : g1, slot, __builtin_amdgcn_readfirstlane(ti), __builtin_amdgcn_readfirstlane(tj), k);
+    gemm_tile<PV, PM, BUF>(db, sel ? g2 : g1, slot, __builtin_amdgcn_readfirstlane(ti), __builtin_amdgcn_readfirstlane(tj), k);
   }
 }
 
@@ -2478,9 +2534,9 @@ __global__ __launch_bounds__(2 * NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))
   const GemmGeom none{OP_NONE, 0, 0, 0};
   leaf9_body(db, o, upd);
   __syncthreads();
-  gemm_unit<false, REV_B>(db, GemmGeom{OP_TRSM, o, 4, 8, upd}, none, slot, half, w, 2);
+  gemm_unit<false, REV_B, false>(db, GemmGeom{OP_TRSM, o, 4, 8, upd}, none, slot, half, w, 2);
   __syncthreads();
-  gemm_unit<false, TRI_A_FIRST>(db, GemmGeom{OP_SYRK, o, 4, 8, upd}, GemmGeom{OP_TT, o, 4, 8, upd}, slot, half, w, 2);
+  gemm_unit<false, TRI_A_FIRST, false>(db, GemmGeom{OP_SYRK, o, 4, 8, upd}, GemmGeom{OP_TT, o, 4, 8, upd}, slot, half, w, 2);
 }
 
 
