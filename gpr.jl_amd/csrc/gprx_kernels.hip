@@ -582,12 +582,12 @@ __device__ __forceinline__ void core_groups() {
     __builtin_amdgcn_sched_group_barrier(0x008, q, 0);
   }
 }
-template <int MODE>
+template <int MODE, bool BUF = true>
 __device__ __forceinline__ void mma_64x64_m(d4 (&acc)[QM][QN], const double* __restrict__ A, size_t lda,
                                             const double* __restrict__ B, size_t ldb, int K) {
   const int nst = __builtin_amdgcn_readfirstlane(K / (4 * Q4SD));  // multiple of 8: K is whole 64-tiles
   if (nst <= 0) return;
-  const CorePtr pa = core_ptr(A, lda), pb = core_ptr(B, ldb);
+  const auto pa = core_addr<BUF>(A, lda), pb = core_addr<BUF>(B, ldb);
   constexpr bool first = MODE == TRI_A_FIRST || MODE == TRI_AB_FIRST;
   constexpr bool last = MODE == TRI_A_LAST || MODE == TRI_B_LAST;
   Frag4 f0, f1;
@@ -2696,8 +2696,10 @@ __device__ __forceinline__ void lauum_unit(const DevBatch& db, int slot, const i
   GTS_L(1 + 3 * gu);
   if (active) {  // wave-uniform: diagonal tiles form only their lower blocks
     const double* Ap = db.Mt + so + (size_t)ti * TS * ld + ti * TS;
-    if (ti == tj) mma_64x64_m<TRI_AB_FIRST>(acc, Ap, ld, Ap, ld, (nt - ti) * TS);
-    else mma_64x64_m<TRI_A_FIRST>(acc, Ap, ld, db.Mt + so + (size_t)ti * TS * ld + tj * TS, ld, (nt - ti) * TS);
+    // global addressing here: the buffer-load form (k_gemm's) measured 0.15 ms slower in this kernel
+    // (11.60 / 11.66 / 11.53 against 11.41 / 11.47 / 11.44 ms, same box, bit-identical output)
+    if (ti == tj) mma_64x64_m<TRI_AB_FIRST, false>(acc, Ap, ld, Ap, ld, (nt - ti) * TS);
+    else mma_64x64_m<TRI_A_FIRST, false>(acc, Ap, ld, db.Mt + so + (size_t)ti * TS * ld + tj * TS, ld, (nt - ti) * TS);
   }
   GTS_L(2 + 3 * gu);
 #ifdef GPRX_STAMPS
