@@ -231,9 +231,9 @@ void factor_rec(gprx_ctx* c, hipStream_t st, const DevBatch& db, int o, int n, i
     const double m = 4 * T;
     timed(c, st, "node8a", Bd * (2.0 * m * m * m / 3.0 + 3.0 * m * m * m), Bd * 8.0 * 4.0 * (2 * m) * (2 * m),
           [&] { gprx::launch_node8(db, o, upd, st); }, n);
-    factor_rec(c, st, db, o + 4, 4, 1);
-    gprx::GemmGeom g{gprx::OP_LINV21, o, 4, 8, upd};
-    timed(c, st, "trtri_linv21", Bd * m * m * m, Bd * 8.0 * (3.0 * m * m + m * m / 2.0), [&] { gprx::launch_gemm(db, g, st); }, n);
+    // the bottom leaf and the node's LINV21 in one launch
+    timed(c, st, "node8b", Bd * (2.0 * m * m * m / 3.0 + m * m * m), Bd * 8.0 * (3.0 * m * m + 3.0 * m * m + m * m / 2.0),
+          [&] { gprx::launch_node8b(db, o, upd, st); }, n);
     return;
   }
   if (n == 1) {

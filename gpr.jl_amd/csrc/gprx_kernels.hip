@@ -2142,8 +2142,29 @@ struct Leaf9Sync {
   int diag_done;   // diagonal tiles factored and inverted
   int tile_ready;  // diagonal tiles handed to wave 0 (tile 0 at the start)
   int xfree;       // steps whose readers of dX[k & 1] are done
+  int crit;        // critical SYRK items done (monotonic over the steps)
 };
 constexpr int L9_TW = 7;
+// position of task wave w in l9_wave_of's round robin (5, 6, 7, 1, 2, 3, 4)
+__device__ __forceinline__ int l9_pos(int w) { return w >= 5 ? w - 5 : (w <= 3 ? w + 2 : 6); }
+// phase B of step k (m = n - 1 - k trailing tiles per edge): the SYRK tiles the next step needs,
+// column k + 1 below the diagonal and the next diagonal tile, are its first nc tiles in the
+// column-major enumeration that skips (k + 1, k + 1)
+__host__ __device__ constexpr int l9_crit_tiles(int m) { return m <= 0 ? 0 : (m - 1) + (m >= 2 ? 1 : 0); }
+__device__ __forceinline__ void lds_wait_ge(const int* p, int v, const DevBatch& db, int slot) {
+  for (int it = 0; lds_load(p) < v; ++it) {
+    if (it > LW_SPIN) {
+      lw_timeout(db, slot);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  l9_acquire();
+}
+__device__ __forceinline__ void lds_count(int* p) {  // one more item done (its stores before the count)
+  l9_release();
+  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(p, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 // Items go round the task waves, the three off the chain first (waves 5, 6, 7, then 1, 2, 3, 4);
 // the diagonal tile's four store quarters go to waves 4..7.
 constexpr int L9_HW = 7;
@@ -2274,6 +2295,7 @@ __device__ __forceinline__ void leaf9_body(const DevBatch& db, int o, int upd) {
       sy.diag_done = 0;
       sy.tile_ready = 1;
       sy.xfree = 0;
+      sy.crit = 0;
     }
   }
   __syncthreads();
@@ -2309,12 +2331,17 @@ __device__ __forceinline__ void leaf9_body(const DevBatch& db, int o, int upd) {
       for (int s = 0; s < 16; ++s) Bs[4 * s * FS + cq + llo] = v[s];
     };
     if (cw >= 0) preload(0);
+    const int rw = l9_pos(wave);
+    int ncrit = 0;  // critical SYRK items of the steps so far (sy.crit's target)
+    int nc4p = 0;   // critical items of the previous step's phase B (the held items' offset)
     for (int k = 0; k < n; ++k) {
       const int kk = o + k;
       const double* Kc = k > 0 ? S : K0;
       const double* dX = dXb + (k & 1) * TS * FS;
-      // items of Y(k, j) held since the previous step: e = 4 j + c, on wave l9_wave_of(e), slot e / 7
+      // items of Y(k, j) held since the previous step: e = 4 j + c, phase-B item g = nc4p + e on
+      // wave l9_wave_of(g); this wave's h-th one is g = g0 + 7 h (g0: its first g >= nc4p)
       const int nyp = 4 * k;  // Y(k, j), j < k
+      const int g0p = nc4p + ((rw - nc4p) % 7 + 7) % 7;
       lds_wait_gt(&sy.diag_done, k, db, slot);
       if (wave == 5) L9_TS(9 + 4 * k);
       // ---- phase A: the chain; the held inverse items of row k; the diagonal tile's stores; the
@@ -2366,9 +2393,8 @@ __device__ __forceinline__ void leaf9_body(const DevBatch& db, int o, int upd) {
       // held items: X(k, j) = -Linv_kk Y(k, j), columns cq.. of tile (kk, o + j)
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const int e0 = h * L9_HW;
-        for (int e = e0; e < e0 + L9_HW && e < nyp; ++e) {
-          if (l9_wave_of(e) != wave) continue;
+        const int e = g0p + 7 * h - nc4p;
+        if (e < nyp) {
           const int j = e >> 2, c = e & 3, tj = o + j, xq = 16 * c;
           double b[16];
 #pragma unroll
@@ -2400,9 +2426,14 @@ __device__ __forceinline__ void leaf9_body(const DevBatch& db, int o, int upd) {
       {
         const int nt1 = n - 2 - k > 0 ? n - 2 - k : 0;
         const int na = 4 + 4 * nt1;
+        bool waited = false;
         for (int e = 0; e < na; ++e) {
           if ((e < 4 ? 4 + e : l9_wave_of(nyp + e - 4)) != wave) continue;
           const int c = e & 3, xq = 16 * c;
+          if (e >= 4 && !waited) {  // S(ti, kk): the previous step's critical items
+            lds_wait_ge(&sy.crit, ncrit, db, slot);
+            waited = true;
+          }
           if (e < 4) {  // columns xq.. of the diagonal tile: Linv, Mt = Linv^T, z partial
             double* Lc = Li + (size_t)kk * TS * ld + kk * TS;
             double* Mc = Mt + (size_t)kk * TS * ld + kk * TS;
@@ -2441,31 +2472,23 @@ __device__ __forceinline__ void leaf9_body(const DevBatch& db, int o, int upd) {
         L9_TS(11 + 4 * k);
       }
       if (k == n - 1) break;
-      // ---- phase B: Y(k+1, j) for j <= k (held), then the SYRK rows of the trailing tiles
-      //      other than (kk+1, kk+1)
+      // ---- phase B (round 5: no closing barrier): items in the order the next step needs them,
+      //      g = 0.. on wave l9_wave_of(g):
+      //        the critical SYRK rows (column kk+1 below the diagonal and tile (kk+2, kk+2): the next
+      //        step's chain and TRSMs read them, after sy.crit counts them);
+      //        Y(k+1, j), j <= k (held for the next phase A);
+      //        the other SYRK rows (read only after the next phase A's barrier).
+      //      The chain waves then wait for the critical count and stage the next chain operand.
       {
         const int k1 = kk + 1;
         const int ny = 4 * (k + 1);
-        [[maybe_unused]] int nb = 0;
-        W_TS(8 * k);
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int e0 = h * L9_HW;
-          for (int e = e0; e < e0 + L9_HW && e < ny; ++e) {
-            if (l9_wave_of(e) != wave) continue;
-            const int j = e >> 2, c = e & 3, tj = o + j, xq = 16 * c;
-            // Y(k1, tj)[:, xq..] = sum_{m=tj}^{kk} L(k1, m) Linv(m, tj): M = Lw row k1, N = Mt row tj
-            // (Linv(m, tj)^T); Linv(tj, tj)'s columns xq.. are zero above row xq: K starts at xq
-            acc_zero4(yh[h]);
-            mma_rd(yh[h], Lw + (size_t)(tj * TS + xq) * ld + k1 * TS, ld, Mt + (size_t)(tj * TS + xq) * ld + tj * TS + xq, ld,
-                   (k1 - tj) * TS - xq);
-            W_TS(8 * k + 1 + (nb < 5 ? nb++ : 5));
-          }
-        }
         const int m = n - 1 - k;  // trailing tiles per edge
         const int nsy = m * (m + 1) / 2 - 1;
-        for (int e = 0; e < 4 * nsy; ++e) {
-          if (l9_wave_of(ny + e) != wave) continue;
+        const int nc4 = 4 * l9_crit_tiles(m);
+        [[maybe_unused]] int nb = 0;
+        W_TS(8 * k);
+        // SYRK row item e (tile e / 4 of the enumeration, quarter e % 4)
+        auto syrk_item = [&](int e) {
           const int c = e & 3, xq = 16 * c;
           int u = (e >> 2) + 1, cc = 0;  // lower trailing tile u (column-major), skipping (k1, k1)
           while (u >= m - cc) {
@@ -2486,12 +2509,35 @@ __device__ __forceinline__ void leaf9_body(const DevBatch& db, int o, int upd) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) S[(tj * TS + 16 * a + 4 * q) * ldi + ti * TS + xq + lo] = -acc[a][q];
           W_TS(8 * k + 1 + (nb < 5 ? nb++ : 5));
+        };
+        for (int g = (rw - 0 + 7) % 7; g < nc4; g += 7) {
+          syrk_item(g);
+          lds_count(&sy.crit);
         }
+        const int g0 = nc4 + ((rw - nc4) % 7 + 7) % 7;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int e = g0 + 7 * h - nc4;
+          if (e < ny) {
+            const int j = e >> 2, c = e & 3, tj = o + j, xq = 16 * c;
+            // Y(k1, tj)[:, xq..] = sum_{m=tj}^{kk} L(k1, m) Linv(m, tj): M = Lw row k1, N = Mt row tj
+            // (Linv(m, tj)^T); Linv(tj, tj)'s columns xq.. are zero above row xq: K starts at xq
+            acc_zero4(yh[h]);
+            mma_rd(yh[h], Lw + (size_t)(tj * TS + xq) * ld + k1 * TS, ld, Mt + (size_t)(tj * TS + xq) * ld + tj * TS + xq, ld,
+                   (k1 - tj) * TS - xq);
+            W_TS(8 * k + 1 + (nb < 5 ? nb++ : 5));
+          }
+        }
+        for (int g = nc4 + ny + ((rw - nc4 - ny) % 7 + 7) % 7; g < 4 * nsy + ny; g += 7) syrk_item(g - ny);
         W_TS(8 * k + 7);
+        ncrit += nc4;
+        nc4p = nc4;
       }
-      ctr_barrier(&sy.tk, gen, L9_TW, db, slot);
       if (wave == 5) L9_TS(12 + 4 * k);
-      if (cw >= 0 && k + 1 < n - 1) preload(k + 1);
+      if (cw >= 0 && k + 1 < n - 1) {
+        lds_wait_ge(&sy.crit, ncrit, db, slot);  // S(kk+2, kk+1) and S(kk+2, kk+2) for the chain
+        preload(k + 1);
+      }
     }
   }
   __syncthreads();
@@ -2537,6 +2583,20 @@ __global__ __launch_bounds__(2 * NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))
   gemm_unit<false, REV_B, false>(db, GemmGeom{OP_TRSM, o, 4, 8, upd}, none, slot, half, w, 2);
   __syncthreads();
   gemm_unit<false, TRI_A_FIRST, false>(db, GemmGeom{OP_SYRK, o, 4, 8, upd}, GemmGeom{OP_TT, o, 4, 8, upd}, slot, half, w, 2);
+}
+// The second half of an 8-tile node (round 5): its bottom leaf (leaf9_body at o + 4, tiles
+// updated into S) and then its LINV21 (L^-1_21 = -L22^-1 T) in one launch, one 8-wave workgroup
+// per slot: the node's two LINV21 units run on the two halves of the workgroup (5 tile-K per wave
+// after the fold, instead of a separate launch of 2 workgroups per slot).  The transposed Mt store
+// of LINV21 uses the leaf's LDS, dead after its barrier.
+__global__ __launch_bounds__(2 * NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_node9b(DevBatch db, int o, int upd) {
+  const int slot = blockIdx.x;
+  if (slot >= db.B || !slot_active(db, slot)) return;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), half = wave >> 2, w = wave & 3;
+  const GemmGeom none{OP_NONE, 0, 0, 0};
+  leaf9_body(db, o + 4, 1);
+  __syncthreads();
+  gemm_unit<false, REV_A, false>(db, GemmGeom{OP_LINV21, o, 4, 8, upd}, none, slot, half, w, 2);
 }
 
 
@@ -3232,7 +3292,7 @@ void set_kernel_attributes() {
   (void)hipFuncSetAttribute((const void*)k_lauum_grad, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   for (const void* f : {(const void*)k_pred_cross<0>, (const void*)k_pred_cross<1>})
     (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)cross_lds(DMAX));
-  for (const void* f : {(const void*)k_leaf9, (const void*)k_node9})
+  for (const void* f : {(const void*)k_leaf9, (const void*)k_node9, (const void*)k_node9b})
     (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)leaf9_lds_bytes());
   set_lbfgs_attributes();
 }
@@ -3259,6 +3319,9 @@ void launch_leaf(const DevBatch& b, int o, int n, int upd, hipStream_t s) {
 }
 void launch_node8(const DevBatch& b, int o, int upd, hipStream_t s) {
   hipLaunchKernelGGL(k_node9, dim3(b.B), dim3(2 * NTHR), leaf9_lds_bytes(), s, b, o, upd);
+}
+void launch_node8b(const DevBatch& b, int o, int upd, hipStream_t s) {
+  hipLaunchKernelGGL(k_node9b, dim3(b.B), dim3(2 * NTHR), leaf9_lds_bytes(), s, b, o, upd);
 }
 void launch_gemm(const DevBatch& b, const GemmGeom& g, hipStream_t s, const GemmGeom& g2) {
   if (g.op != OP_PREDVAR && g.n <= b.small_n) {  // small node: pair units, 64 x 32 waves
