@@ -74,4 +74,12 @@ for leaf in range(8):
                 rel = (t - ts[leaf][:, :1]) / 100.0
                 ph[f"s{k}_w{wv}"] = [round(float(np.median(rel[:, i])), 1) if (t[:, i] > 0).all() else None for i in range(8)]
         out[f"leaf{leaf}_phaseB"] = ph
+        # round 5: step 0 per wave: 24 phase A start, 25 after the chain, 26 A items done, 27 after
+        # the A barrier, 28 first B item's C loaded, 29 its products done (stamps build waits)
+        a0 = {}
+        for wv in range(1, 8):
+            t = w[:, wv, 24:30]
+            rel = (t - ts[leaf][:, :1]) / 100.0
+            a0[f"w{wv}"] = [round(float(np.median(rel[:, i])), 1) if (t[:, i] > 0).all() else None for i in range(6)]
+        out[f"leaf{leaf}_A0"] = a0
 print(json.dumps(out, indent=1), flush=True)

@@ -7,3 +7,5 @@ tail -n 2 gpurun_out/la_tests.txt
 REPS=2 bash scratch/ab_bits.sh scratch/var/libgprx_prev.so
 timeout -k 10 200 python scratch/levels.py 40 3 > gpurun_out/la_levels.txt 2>&1
 cat gpurun_out/la_levels.txt | grep -v amdgpu.ids
+GPRX_LIB=scratch/var/libgprx_stamps.so timeout -k 10 300 python scratch/leaf8_timeline.py 40 > gpurun_out/la_tl.json 2>&1
+echo timeline ok

@@ -103,6 +103,93 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   out[blockIdx.x * 256 + threadIdx.x] = t;
 }
 
+// V7: the library core's pattern: 2 stages of 8 A + 8 B fragment loads (global, 64-bit VGPR
+// addresses advanced per stage) in ping-pong with 32 MFMAs each, over an L2-resident panel;
+// V8: the same with buffer loads (32-bit lane offset in a VGPR, stage offset in an SGPR)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes, 0x00020000);
+}
+template <int V>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_core(const double* P, double* out, int iters) {
+  constexpr int LD = 256;  // panel: 256 x 64 doubles (128 KB), column-major, L2-resident
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  d4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = (d4){0, 0, 0, 0};
+  double fa[2][2][4], fb[2][2][4];  // [buffer][substep][block]
+  const __amdgpu_buffer_rsrc_t r = rsrc(P, LD * 64 * 8);
+  const int vo = (lr + lk * LD) * 8;
+  auto load = [&](int buf, int st) {
+    const int stage = st & 3;  // wrap over the panel's 64 columns (8 per stage)
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        if constexpr (V == 7) {
+          const double* p = P + lr + lk * LD + (stage * 8 + 4 * s) * LD;
+          fa[buf][s][a] = p[16 * a];
+          fb[buf][s][a] = p[64 + 16 * a];
+        } else {
+          const int so = (stage * 8 + 4 * s) * LD * 8;
+          fa[buf][s][a] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, vo + 128 * a, so, 0));
+          fb[buf][s][a] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, vo + 512 + 128 * a, so, 0));
+        }
+      }
+  };
+  auto mm = [&](int buf) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = mfma(fb[buf][s][b], fa[buf][s][a], acc[a][b]);
+  };
+  load(0, 0);
+  for (int it = 0; it < iters; it += 2) {
+    __builtin_amdgcn_sched_barrier(0);
+    load(1, it + 1);
+    mm(0);
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    load(0, it + 2);
+    mm(1);
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  double t = 0.0;
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) t += acc[a][b][0] + acc[a][b][3];
+  out[blockIdx.x * 256 + threadIdx.x] = t;
+}
+template <int V>
+void run_core(const double* src, double* out, int iters, const char* name) {
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  for (int r = 0; r < 3; ++r) hipLaunchKernelGGL(k_core<V>, dim3(512), dim3(256), 0, 0, src, out, iters);
+  (void)hipEventRecord(e0);
+  for (int r = 0; r < 5; ++r) hipLaunchKernelGGL(k_core<V>, dim3(512), dim3(256), 0, 0, src, out, iters);
+  (void)hipEventRecord(e1);
+  (void)hipEventSynchronize(e1);
+  float ms;
+  (void)hipEventElapsedTime(&ms, e0, e1);
+  ms /= 5;
+  const double fl = 512.0 * 4 * 32 * 2048.0 * iters;  // 32 MFMAs per stage, one stage per iteration
+  printf("%-48s %8.3f ms  %6.2f TF/s\n", name, ms, fl / (ms * 1e-3) / 1e12);
+}
+
 template <int V>
 void run(const double* src, double* out, int iters, const char* name) {
   hipEvent_t e0, e1;
@@ -135,6 +222,11 @@ int main() {
   run<4>(src, out, it, "V4 V3 + sched_group_barrier interleave");
   run<5>(src, out, it, "V5 V1 + 8 int VALU per 16 MFMAs");
   run<6>(src, out, it, "V6 V1 + 16 int VALU per 16 MFMAs");
+  double* panel;
+  (void)hipMalloc(&panel, 256 * 64 * 8);
+  (void)hipMemset(panel, 0, 256 * 64 * 8);
+  run_core<7>(panel, out, it, "V7 core: global loads, 64-bit VGPR addresses");
+  run_core<8>(panel, out, it, "V8 core: buffer loads, SGPR stage offsets");
   printf("err=%s\n", hipGetErrorString(hipGetLastError()));
   return 0;
 }
