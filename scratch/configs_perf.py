@@ -1,6 +1,6 @@
 """fits/s of the four BASELINE configurations (fit = Gram+Cholesky+alpha+LML, full gradient,
 mean+variance at M=100), one batch per call, and the algorithmic TF/s of each (bench.fit_flops).
-    python scratch/configs_perf.py [out.json]"""
+    python scratch/configs_perf.py [out.json] [--cp T1,T2,...]   (--cp: only CP at those trial counts)"""
 import json
 import pathlib
 import sys
@@ -17,6 +17,10 @@ from gprx import data  # noqa: E402
 ctx = gprx.Context(0)
 cases = [("P1", 50, 64, 3, 256), ("CP", 512, 512, 26, 8), ("CP", 512, 512, 26, 16), ("CP", 512, 512, 26, 24),
          ("CP", 512, 512, 26, 32), ("P2", 2048, 2048, 6, 40), ("FB", 4096, 512, 12, 4), ("FB", 4096, 512, 12, 8)]
+if "--cp" in sys.argv:
+    i = sys.argv.index("--cp")
+    cases = [("CP", 512, 512, 26, int(t)) for t in sys.argv[i + 1].split(",")]
+    del sys.argv[i:i + 2]
 rows = []
 for mech, N, key, G, trials in cases:
     trs = [data.make_trial(mech, N, 100, seed=data.trial_seed(mech, t)) for t in range(trials)]
