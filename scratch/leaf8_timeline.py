@@ -50,6 +50,10 @@ for leaf in range(8):
     if not (t[:, 0] > 0).all():
         continue
     row = {names[e]: round(float(np.median((t[:, e] - t[:, 0]) / 100.0)), 2) for e in sorted(names) if (t[:, e] > 0).all()}
+    # the launch's spread: slots' start and end against the earliest start of the launch (us)
+    t0 = t[:, 0].min()
+    row["abs_start_p50_max"] = [round(float(np.percentile((t[:, 0] - t0) / 100.0, q)), 2) for q in (50, 100)]
+    row["abs_end_p10_p50_p90_max"] = [round(float(np.percentile((t[:, 25] - t0) / 100.0, q)), 2) for q in (10, 50, 90, 100)]
     out[f"leaf{leaf}"] = row
     # the diagonal routine's phases per tile (durations, us): zero, then per P factor / TRSM / SYRK,
     # inverse off-diagonal blocks, logdet
