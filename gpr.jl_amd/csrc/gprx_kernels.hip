@@ -641,25 +641,44 @@ __device__ __forceinline__ void mma_64x64_m(d4 (&acc)[QM][QN], const double* __r
 // K backward from their lower-triangular last tile (Linv[tj,tj], Linv[ti,ti]: reversed trip T
 // needs the row / column blocks >= 3 - T).  tri: this wave's op is PM's.
 template <int PM, bool BUF = true>
-__device__ __forceinline__ void mma_64x64_pm(d4 (&acc)[QM][QN], const double* __restrict__ A, size_t lda,
-                                             const double* __restrict__ B, size_t ldb, int K, bool tri) {
+__device__ __forceinline__ void mma_64x64_pm(d4 (&acc)[QM][QN], Frag4& f0, const double* __restrict__ A, size_t lda,
+                                             const double* __restrict__ B, size_t ldb, int K, bool tri, bool pre, bool nxt,
+                                             const double* nA, const double* nB, int nK) {
+  // pre: f0 already holds this tile's first stage (loaded by the previous tile's last iteration);
+  // nxt: the last iteration loads the next tile's first stage (operands nA, nB, K range nK, the
+  // same op and walk) into f0 instead of re-reading its own last stage, so the next tile's first
+  // MFMAs do not wait for a load issued after this tile's epilogue (round 5)
   const int nst = __builtin_amdgcn_readfirstlane(K / (4 * Q4SD));
   if (nst <= 0) return;
   auto pa = core_addr<BUF>(A, lda), pb = core_addr<BUF>(B, ldb);
-  Frag4 f0, f1;
+  Frag4 f1;
   int it = 0;
   if (tri) {
     if constexpr (PM == REV_A || PM == REV_B) {  // stage j reads the k of stage nst - 1 - j
       pa = core_rev(pa, nst);
       pb = core_rev(pb, nst);
     }
-    core_load<PM, 0>(f0, pa, pb, 0);
+    if (!pre) core_load<PM, 0>(f0, pa, pb, 0);
     GPRX_TRIP(PM, 0, 1, 0, true)
     GPRX_TRIP(PM, 1, 2, 2, true)
     GPRX_TRIP(PM, 2, 3, 4, true)
     it = 6;
   } else {
-    core_load<PLAIN, 4>(f0, pa, pb, 0);
+    if (!pre) core_load<PLAIN, 4>(f0, pa, pb, 0);
+  }
+  [[maybe_unused]] auto na = pa, nb = pb;
+  if constexpr (BUF) {
+    if (nxt) {
+      const int nn = __builtin_amdgcn_readfirstlane(nK / (4 * Q4SD));
+      na = core_addr<BUF>(nA, lda);
+      nb = core_addr<BUF>(nB, ldb);
+      if constexpr (PM == REV_A || PM == REV_B) {
+        if (tri) {
+          na = core_rev(na, nn);
+          nb = core_rev(nb, nn);
+        }
+      }
+    }
   }
   for (; it < nst; it += 2) {
     __builtin_amdgcn_sched_barrier(0);
@@ -668,7 +687,19 @@ __device__ __forceinline__ void mma_64x64_pm(d4 (&acc)[QM][QN], const double* __
     core_groups<PLAIN>();
     __builtin_amdgcn_sched_barrier(0);
     const int n2 = (it + 2 < nst) ? it + 2 : nst - 1;
-    core_load<PLAIN, 4>(f0, pa, pb, n2);
+    if constexpr (BUF) {
+      const bool nx = nxt && it + 2 >= nst;  // wave-uniform: scalar selects, no branch
+      CorePtr la = pa, lb = pb;
+      la.r = nx ? na.r : pa.r;
+      la.o = nx ? na.o : pa.o + n2 * pa.st;
+      la.sub = nx ? na.sub : pa.sub;
+      lb.r = nx ? nb.r : pb.r;
+      lb.o = nx ? nb.o : pb.o + n2 * pb.st;
+      lb.sub = nx ? nb.sub : pb.sub;
+      core_load<PLAIN, 4>(f0, la, lb, 0);
+    } else {
+      core_load<PLAIN, 4>(f0, pa, pb, n2);
+    }
     core_mma<PLAIN, 4>(acc, f1);
     core_groups<PLAIN>();
     __builtin_amdgcn_sched_barrier(0);
@@ -1299,10 +1330,15 @@ __device__ __forceinline__ void diag_store(const DevBatch& db, int slot, int jt,
 // ============================================================================================
 // One 64 x 64 output tile (ti, tj) of a GemmOp on one wave.
 constexpr int TT_S = TS + 2;  // row stride of k_gemm's per-wave transpose buffer (LINV21's Mt store)
-template <bool PV, int PM = PLAIN, bool BUF = true>
-__device__ __forceinline__ void gemm_tile(const DevBatch& db, const GemmGeom& g, int slot, int ti, int tj, int pass = 0) {
-  GTS(g, pass, 0);
-  const int op = PV ? (int)OP_PREDVAR : g.op;
+constexpr size_t linv21_lds_bytes() { return (size_t)4 * 32 * TT_S * sizeof(double); }  // 4 waves x [32][66]
+// operands of tile (ti, tj) of a GemmOp: A and B at the K range's start, B's leading dimension,
+// the K range (elements)
+struct TileOps {
+  const double *A, *B;
+  size_t ldb;
+  int Kn;
+};
+__device__ __forceinline__ TileOps tile_ops(const DevBatch& db, int op, const GemmGeom& g, int slot, int ti, int tj) {
   const size_t ld = db.ld, so = (size_t)slot * db.mat;
   int kb, ke;  // K range in tiles
   const double *A, *Bm;
@@ -1320,6 +1356,18 @@ __device__ __forceinline__ void gemm_tile(const DevBatch& db, const GemmGeom& g,
       ldb = db.Mpad;
       break;
   }
+  return TileOps{A + (size_t)kb * TS * ld + ti * TS, Bm + (size_t)kb * TS * ldb + tj * TS, ldb, (ke - kb) * TS};
+}
+// f0 / pre / nxt / (nti, ntj): the register stage handed from one tile of a wave's folded pair to
+// the next (mma_64x64_pm)
+template <bool PV, int PM = PLAIN, bool BUF = true>
+__device__ __forceinline__ void gemm_tile(const DevBatch& db, const GemmGeom& g, int slot, int ti, int tj, int pass, Frag4& f0,
+                                          bool pre, bool nxt, int nti, int ntj) {
+  GTS(g, pass, 0);
+  const int op = PV ? (int)OP_PREDVAR : g.op;
+  const size_t ld = db.ld, so = (size_t)slot * db.mat;
+  const TileOps to = tile_ops(db, op, g, slot, ti, tj);
+  const size_t ldb = to.ldb;
   const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
   // the output tile's addressing (the SYRK's C and every op's stores): buffer ops over the tile,
   // the lane's byte offset per q in a VGPR, the 16-column block b in an SGPR, the row block a in the
@@ -1338,24 +1386,25 @@ __device__ __forceinline__ void gemm_tile(const DevBatch& db, const GemmGeom& g,
   } else {
     acc4_zero(acc);
   }
-  const double* Ak = A + (size_t)kb * TS * ld + ti * TS;
-  const double* Bk = Bm + (size_t)kb * TS * ldb + tj * TS;
+  const double* Ak = to.A;
+  const double* Bk = to.B;
   if constexpr (PV) {  // prediction (own kernel instance): skip the last test tile's all-padding blocks
     const int nbv = __builtin_amdgcn_readfirstlane((db.M - tj * TS + 15) >> 4);
-    if (nbv >= QN) mma_64x64(acc, Ak, ld, Bk, ldb, (ke - kb) * TS);
-    else if (nbv == 3) mma_64x64<3>(acc, Ak, ld, Bk, ldb, (ke - kb) * TS);
-    else if (nbv == 2) mma_64x64<2>(acc, Ak, ld, Bk, ldb, (ke - kb) * TS);
-    else mma_64x64<1>(acc, Ak, ld, Bk, ldb, (ke - kb) * TS);
+    if (nbv >= QN) mma_64x64(acc, Ak, ld, Bk, ldb, to.Kn);
+    else if (nbv == 3) mma_64x64<3>(acc, Ak, ld, Bk, ldb, to.Kn);
+    else if (nbv == 2) mma_64x64<2>(acc, Ak, ld, Bk, ldb, to.Kn);
+    else mma_64x64<1>(acc, Ak, ld, Bk, ldb, to.Kn);
   } else {
 #ifdef GPRX_STAMPS
     const Stamp st0 = stamp_now();
 #endif
     // the operands' triangular tiles (diagonal tiles of Linv / Mt) and SYRK's upper blocks of a
     // diagonal tile are skipped (mma_64x64_m); op and ti == tj are wave-uniform
-    const int Kn = (ke - kb) * TS;
     const bool tri = (PM == TRI_A_FIRST && op == OP_TT) || (PM == REV_A && op == OP_LINV21) || (PM == REV_B && op == OP_TRSM);
+    TileOps tn = to;
+    if (nxt) tn = tile_ops(db, op, g, slot, nti, ntj);
     GTS(g, pass, 1);
-    mma_64x64_pm<PM, BUF>(acc, Ak, ld, Bk, ldb, Kn, tri);
+    mma_64x64_pm<PM, BUF>(acc, f0, Ak, ld, Bk, ldb, to.Kn, tri, pre, nxt, tn.A, tn.B, tn.Kn);
     GTS(g, pass, 2);
 #ifdef GPRX_STAMPS
     if ((op == OP_SYRK || op == OP_TT) && g.n == db.nt) {
@@ -1406,22 +1455,42 @@ __device__ __forceinline__ void gemm_tile(const DevBatch& db, const GemmGeom& g,
       for (int q = 0; q < 4; ++q) buffer_store_f64(crw, vl + 128 * a, (16 * b + 4 * q) * Lb, acc[a][b][q]);
   if (op == OP_LINV21) zp_acc4(db, slot, ti, tj, acc, 1.0);
   if (op != OP_LINV21) GTS(g, pass, 3);
-  if (op == OP_LINV21) {  // Mt[tj, ti] = Linv[ti, tj]^T, transposed through LDS 16 rows at a time
-    // so that every store instruction writes one contiguous 512-B column segment of Mt
+  if (op == OP_LINV21) {  // Mt[tj, ti] = Linv[ti, tj]^T, transposed through LDS 32 rows at a time
+    // (round 5: two rounds instead of four 16-row ones, and 16-B reads and stores: every store
+    // instruction writes two contiguous 512-B column segments of Mt)
     extern __shared__ __attribute__((aligned(16))) double gsm[];
-    // this wave's [16][66] buffer: at row stride 66 the 16 x 4 lanes of a store write 64 distinct
-    // banks per half-wave (stride 65 put lanes with equal lr + lk in one bank)
-    double* tb = gsm + (threadIdx.x >> 6) * (16 * TT_S);
+    // this wave's [32][66] buffer: at row stride 66 the 16 x 4 lanes of a write hit 64 distinct
+    // banks per half-wave (stride 65 put lanes with equal lr + lk in one bank); 528-B rows keep the
+    // 16-B reads aligned
+    double* tb = gsm + (threadIdx.x >> 6) * (32 * TT_S);
     double* Mtt = db.Mt + so + (size_t)(ti * TS) * ld + tj * TS;
+    const int hr = l >> 5, c2 = 2 * (l & 31);  // 16-B lane: row parity, column pair
+    const int vst = (hr * (int)ld + c2) * (int)sizeof(double);
 #pragma unroll
-    for (int a = 0; a < QM; ++a) {
+    for (int h = 0; h < 2; ++h) {
 #pragma unroll
-      for (int b = 0; b < QN; ++b)
+      for (int aa = 0; aa < 2; ++aa)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) tb[lr * TT_S + 16 * b + lk + 4 * q] = acc[a][b][q];
+        for (int b = 0; b < QN; ++b)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) tb[(16 * aa + lr) * TT_S + 16 * b + lk + 4 * q] = acc[2 * h + aa][b][q];
       __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) Mtt[(size_t)(16 * a + r) * ld + l] = tb[r * TT_S + l];
+      for (int r2 = 0; r2 < 16; ++r2) {
+        // rows 32h + 2 r2 .. + 1: the pair's base in the resource (SGPRs), the lane's row parity and
+        // column pair in the VGPR offset (soffset 0: see buffer_store_f64x2)
+        const double2 v = *(const double2*)(tb + (2 * r2 + hr) * TT_S + c2);
+        buffer_store_f64x2(buffer_rsrc(Mtt + (size_t)(32 * h + 2 * r2) * ld, 0x7ffffff0), vst, v.x, v.y);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+#pragma unroll
+      for (int g = 0; g < 14; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x040, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x040, 2, 0);
+      __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_wave_barrier();
     }
     GTS(g, pass, 3);
@@ -1498,9 +1567,16 @@ __device__ __forceinline__ void gemm_unit(const DevBatch& db, const GemmGeom& g1
       }
     }
   }
+  // the register stage handed from tile k to tile k + 1 (mma_64x64_pm), in the SYRK + TT instance:
+  // syrk_tt 9.97-10.04 -> 9.84-9.90 ms; TRSM 4.93-4.97 -> 5.03-5.09 and LINV21 unchanged (same-box
+  // A/B, scratch/gemm_ab.sh), so those keep the reload
+  Frag4 f0;
+  bool pre = false;  // f0 holds this tile's first stage
 #pragma unroll 1
   for (int k = 0; k < np; ++k) {
     int sel, ti, tj;
+    bool nxt = false;  // the next tile of the fold exists on this wave: prefetch its first stage
+    int nti = 0, ntj = 0;
     if (plan) {
       const int e = N8_PLAN[w8][k];
       if (e < 0) break;
@@ -1513,9 +1589,16 @@ __device__ __forceinline__ void gemm_unit(const DevBatch& db, const GemmGeom& g1
       sel = sel0;
       ti = r0 + ur + wr;
       tj = c0 + uc + wc;
+      if (!PV && BUF && PM == TRI_A_FIRST && k + 1 < np && pr2 + wr < R && pc2 + wc < C) {  // TT's folds (see below)
+        nxt = true;
+        nti = r0 + pr2 + wr;
+        ntj = c0 + pc2 + wc;
+      }
     }
     // wave-uniform tile indices in SGPRs (the 64 x 64 core needs every VGPR)
-    gemm_tile<PV, PM, BUF>(db, sel ? g2 : g1, slot, __builtin_amdgcn_readfirstlane(ti), __builtin_amdgcn_readfirstlane(tj), k);
+    gemm_tile<PV, PM, BUF>(db, sel ? g2 : g1, slot, __builtin_amdgcn_readfirstlane(ti), __builtin_amdgcn_readfirstlane(tj), k, f0,
+                           pre, nxt, __builtin_amdgcn_readfirstlane(nti), __builtin_amdgcn_readfirstlane(ntj));
+    pre = nxt;
   }
 }
 
@@ -2565,6 +2648,8 @@ __device__ __forceinline__ void leaf9_body(const DevBatch& db, int o, int upd) {
 constexpr size_t leaf9_lds_bytes() {
   return (4 * TS * FS + 10 * 4 * TS + 2 * TS) * sizeof(double) + sizeof(Leaf9Sync);
 }
+// k_node9b's LINV21 epilogue puts its eight waves' transpose buffers in the leaf's LDS
+static_assert(leaf9_lds_bytes() >= 2 * linv21_lds_bytes(), "k_node9b: LINV21 transpose buffers exceed the leaf's LDS");
 __global__ __launch_bounds__(2 * NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_leaf9(DevBatch db, int o, int upd) {
   leaf9_body(db, o, upd);
 }
@@ -3294,6 +3379,8 @@ void set_kernel_attributes() {
     (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)cross_lds(DMAX));
   for (const void* f : {(const void*)k_leaf9, (const void*)k_node9, (const void*)k_node9b})
     (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)leaf9_lds_bytes());
+  for (const void* f : {(const void*)k_gemm<REV_A>, (const void*)k_gemm<REV_B>, (const void*)k_gemm<TRI_A_FIRST>})
+    (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)linv21_lds_bytes());
   set_lbfgs_attributes();
 }
 
@@ -3333,7 +3420,7 @@ void launch_gemm(const DevBatch& b, const GemmGeom& g, hipStream_t s, const Gemm
   int T = op_units(g, b.nt, b.mt);
   if (g2.op != OP_NONE) T += op_units(g2, b.nt, b.mt);
   if (n8_plan(g, g2)) T = 2;  // gemm_body's fixed plan
-  const size_t lds = (g.op == OP_LINV21 || g2.op == OP_LINV21) ? 4 * 16 * TT_S * sizeof(double) : 0;
+  const size_t lds = (g.op == OP_LINV21 || g2.op == OP_LINV21) ? linv21_lds_bytes() : 0;
   if (g.op == OP_PREDVAR) hipLaunchKernelGGL(k_gemm_pv, dim3(grid_blocks(b.B, T)), dim3(NTHR), lds, s, b, g, g2);
   else if (g.op == OP_TRSM) hipLaunchKernelGGL(k_gemm<REV_B>, dim3(grid_blocks(b.B, T)), dim3(NTHR), lds, s, b, g, g2);
   else if (g.op == OP_LINV21) hipLaunchKernelGGL(k_gemm<REV_A>, dim3(grid_blocks(b.B, T)), dim3(NTHR), lds, s, b, g, g2);
