@@ -69,7 +69,7 @@ def make_workload(trials_per_gpu: int, rank: int, world: int):
 
 
 # library stat name -> kernel symbol (prefix) in rocprofv3 output; k_gemm serves several stats
-SYMBOL = {"gram": "k_gram", "leaf": "k_leaf", "node8a": "k_node9", "node8b": "k_node9b", "diag": "k_diag", "alpha": "k_alpha", "lauum_grad": "k_lauum_grad",
+SYMBOL = {"gram": "k_gram", "leaf": "k_leaf", "node8": "k_node8", "diag": "k_diag", "alpha": "k_alpha", "lauum_grad": "k_lauum_grad",
           "finalize": "k_finalize", "pred_cross": "k_pred_cross", "pred_final": "k_pred_final", "pred_var": "k_gemm_pv"}
 
 
@@ -148,7 +148,7 @@ def roofline_parts(kern: dict, nprof: int, global_batch: int) -> dict:
         gram["binding_limit"] = "valu"
         gram["valu_floor"] = pmc_field("gram", global_batch, ("valu_floor_ms", "valu_floor_frac", "clock_ghz_est"))
     return {"gram": gram,
-            "factorisation": part(["leaf", "node8a", "node8b", "diag", "potrf_trsm", "syrk_tt", "trtri_linv21"], "mfma"),
+            "factorisation": part(["leaf", "node8", "diag", "potrf_trsm", "syrk_tt", "trtri_linv21"], "mfma"),
             "lauum_grad": part(["lauum_grad"], "mfma"),
             "pred_var": part(["pred_var"], "mfma")}
 
@@ -436,7 +436,7 @@ def main():
         for _ in range(nprof):
             rb.evaluate(TH)
         ctx.set_profiling(False)
-        names = ["gram", "leaf", "node8a", "node8b", "diag", "potrf_trsm", "syrk_tt", "trtri_linv21", "alpha", "lauum_grad",
+        names = ["gram", "leaf", "node8", "diag", "potrf_trsm", "syrk_tt", "trtri_linv21", "alpha", "lauum_grad",
                  "finalize", "pred_cross", "pred_var", "pred_final"]
         for nme in names:
             kern[nme] = ctx.kernel_stats(nme)

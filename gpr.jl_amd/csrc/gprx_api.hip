@@ -227,13 +227,10 @@ void factor_rec(gprx_ctx* c, hipStream_t st, const DevBatch& db, int o, int n, i
 #ifndef GPRX_NODE8
 #define GPRX_NODE8 1
 #endif
-  if (GPRX_NODE8 && n == 8 && leaf == 4 && db.B >= 32) {  // top leaf + TRSM + SYRK + TT in one launch
+  if (GPRX_NODE8 && n == 8 && leaf == 4 && db.B >= 32) {  // the whole node in one launch (k_node8)
     const double m = 4 * T;
-    timed(c, st, "node8a", Bd * (2.0 * m * m * m / 3.0 + 3.0 * m * m * m), Bd * 8.0 * 4.0 * (2 * m) * (2 * m),
+    timed(c, st, "node8", Bd * (4.0 * m * m * m / 3.0 + 4.0 * m * m * m), Bd * 8.0 * (16.0 * m * m + 6.5 * m * m),
           [&] { gprx::launch_node8(db, o, upd, st); }, n);
-    // the bottom leaf and the node's LINV21 in one launch
-    timed(c, st, "node8b", Bd * (2.0 * m * m * m / 3.0 + m * m * m), Bd * 8.0 * (3.0 * m * m + 3.0 * m * m + m * m / 2.0),
-          [&] { gprx::launch_node8b(db, o, upd, st); }, n);
     return;
   }
   if (n == 1) {

@@ -446,7 +446,7 @@ __device__ __forceinline__ CorePtr core_rev(CorePtr c, int nst) {  // stages and
   c.sub = -c.sub;
   return c;
 }
-// The same walk through 64-bit global addresses (the round-4 form): k_node9 keeps it, since its
+// The same walk through 64-bit global addresses (the round-4 form): k_node8 keeps it, since its
 // GEMM phases sit beside the fused leaf's state and the buffer form's SGPR resources pushed that
 // kernel from 8 to 58 spilled VGPRs.
 struct CorePtrG {
@@ -2648,17 +2648,20 @@ __device__ __forceinline__ void leaf9_body(const DevBatch& db, int o, int upd) {
 constexpr size_t leaf9_lds_bytes() {
   return (4 * TS * FS + 10 * 4 * TS + 2 * TS) * sizeof(double) + sizeof(Leaf9Sync);
 }
-// k_node9b's LINV21 epilogue puts its eight waves' transpose buffers in the leaf's LDS
-static_assert(leaf9_lds_bytes() >= 2 * linv21_lds_bytes(), "k_node9b: LINV21 transpose buffers exceed the leaf's LDS");
+// k_node8's LINV21 epilogue puts its eight waves' transpose buffers in the leaf's LDS
+static_assert(leaf9_lds_bytes() >= 2 * linv21_lds_bytes(), "k_node8: LINV21 transpose buffers exceed the leaf's LDS");
 __global__ __launch_bounds__(2 * NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_leaf9(DevBatch db, int o, int upd) {
   leaf9_body(db, o, upd);
 }
-// The first half of an 8-tile recursion node (512 x 512) in one launch, one 8-wave workgroup per
-// slot: the top leaf (leaf9_body), TRSM and SYRK + TT -- three launches of the recursion with the
-// same tile work, a workgroup barrier between the phases.  The GEMM phases run the slot's units on
-// the two halves of the workgroup (gemm_unit).  (The bottom leaf and LINV21 stay launches of their
-// own: LINV21's epilogue beside the leaf spills.)
-__global__ __launch_bounds__(2 * NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_node9(DevBatch db, int o, int upd) {
+// A whole 8-tile recursion node (512 x 512) in one launch, one 8-wave workgroup per slot, a
+// workgroup barrier between the phases: the top leaf (leaf9_body), TRSM and SYRK + TT, the bottom
+// leaf (tiles updated into S) and LINV21 (L^-1_21 = -L22^-1 T) -- five launches of the recursion
+// with the same tile work.  The GEMM phases run the slot's units on the two halves of the
+// workgroup (gemm_unit); LINV21's transposed Mt store uses the leaf's LDS, dead after its barrier.
+// Round 5: the node's second half joined the first (it was a launch of its own, k_node9b), so each
+// slot goes on to its bottom leaf when its own SYRK + TT is done instead of every slot waiting for
+// the slowest one at the launch boundary: 2.84-2.89 -> 2.79-2.82 ms per step for the four nodes.
+__global__ __launch_bounds__(2 * NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_node8(DevBatch db, int o, int upd) {
   const int slot = blockIdx.x;
   if (slot >= db.B || !slot_active(db, slot)) return;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), half = wave >> 2, w = wave & 3;
@@ -2668,17 +2671,7 @@ __global__ __launch_bounds__(2 * NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))
   gemm_unit<false, REV_B, false>(db, GemmGeom{OP_TRSM, o, 4, 8, upd}, none, slot, half, w, 2);
   __syncthreads();
   gemm_unit<false, TRI_A_FIRST, false>(db, GemmGeom{OP_SYRK, o, 4, 8, upd}, GemmGeom{OP_TT, o, 4, 8, upd}, slot, half, w, 2);
-}
-// The second half of an 8-tile node (round 5): its bottom leaf (leaf9_body at o + 4, tiles
-// updated into S) and then its LINV21 (L^-1_21 = -L22^-1 T) in one launch, one 8-wave workgroup
-// per slot: the node's two LINV21 units run on the two halves of the workgroup (5 tile-K per wave
-// after the fold, instead of a separate launch of 2 workgroups per slot).  The transposed Mt store
-// of LINV21 uses the leaf's LDS, dead after its barrier.
-__global__ __launch_bounds__(2 * NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_node9b(DevBatch db, int o, int upd) {
-  const int slot = blockIdx.x;
-  if (slot >= db.B || !slot_active(db, slot)) return;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), half = wave >> 2, w = wave & 3;
-  const GemmGeom none{OP_NONE, 0, 0, 0};
+  __syncthreads();
   leaf9_body(db, o + 4, 1);
   __syncthreads();
   gemm_unit<false, REV_A, false>(db, GemmGeom{OP_LINV21, o, 4, 8, upd}, none, slot, half, w, 2);
@@ -3377,7 +3370,7 @@ void set_kernel_attributes() {
   (void)hipFuncSetAttribute((const void*)k_lauum_grad, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   for (const void* f : {(const void*)k_pred_cross<0>, (const void*)k_pred_cross<1>})
     (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)cross_lds(DMAX));
-  for (const void* f : {(const void*)k_leaf9, (const void*)k_node9, (const void*)k_node9b})
+  for (const void* f : {(const void*)k_leaf9, (const void*)k_node8})
     (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)leaf9_lds_bytes());
   for (const void* f : {(const void*)k_gemm<REV_A>, (const void*)k_gemm<REV_B>, (const void*)k_gemm<TRI_A_FIRST>})
     (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)linv21_lds_bytes());
@@ -3405,10 +3398,7 @@ void launch_leaf(const DevBatch& b, int o, int n, int upd, hipStream_t s) {
   hipLaunchKernelGGL(k_leaf, dim3(b.B), dim3(NTHR), 0, s, b, o, n, upd);
 }
 void launch_node8(const DevBatch& b, int o, int upd, hipStream_t s) {
-  hipLaunchKernelGGL(k_node9, dim3(b.B), dim3(2 * NTHR), leaf9_lds_bytes(), s, b, o, upd);
-}
-void launch_node8b(const DevBatch& b, int o, int upd, hipStream_t s) {
-  hipLaunchKernelGGL(k_node9b, dim3(b.B), dim3(2 * NTHR), leaf9_lds_bytes(), s, b, o, upd);
+  hipLaunchKernelGGL(k_node8, dim3(b.B), dim3(2 * NTHR), leaf9_lds_bytes(), s, b, o, upd);
 }
 void launch_gemm(const DevBatch& b, const GemmGeom& g, hipStream_t s, const GemmGeom& g2) {
   if (g.op != OP_PREDVAR && g.n <= b.small_n) {  // small node: pair units, 64 x 32 waves

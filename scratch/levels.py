@@ -27,7 +27,7 @@ ctx.reset_stats()
 for _ in range(reps):
     b.run(T, grad=True, predict=True)
 ctx.set_profiling(False)
-names = ["gram", "leaf/n4", "leaf/n2", "node8a/n8", "node8b/n8", "diag"]
+names = ["gram", "leaf/n4", "leaf/n2", "node8/n8", "diag"]
 for op in ("potrf_trsm", "syrk_tt", "trtri_linv21"):
     names += [f"{op}/n{n}" for n in (32, 16, 8, 4, 2)]
 names += ["alpha", "lauum_grad", "finalize", "pred_cross", "pred_var", "pred_mu", "pred_final"]

@@ -381,7 +381,7 @@ def test_factorisation_paths_match_golden(gprx, golden_dir, leaf, small_n):
 
 
 def test_fused_node_failure_isolated(gprx, ctx):
-    """The fused 8-tile node (k_node9: top leaf + TRSM + SYRK+TT, then k_leaf9 for the bottom leaf)
+    """The fused 8-tile node (k_node8: top leaf + TRSM + SYRK+TT + bottom leaf + LINV21 in one launch)
     at B = 32, N = 512: a slot whose point p has NaN coordinates fails at pivot p + 1 (dpotf2's
     first pivot that is not > 0), once in the top leaf (p = 100) and once in the bottom leaf
     (p = 300); every other slot is bit-identical to a run without those slots' NaNs."""
@@ -972,7 +972,7 @@ def test_reproducible_beside_another_gpu_process(gprx, ctx):
 
 
 def test_first_launches_from_concurrent_contexts_in_a_fresh_process(golden_dir):
-    """Kernel attributes (dynamic LDS above 64 KB: k_leaf9 / k_node9 151 KB, k_lauum_grad, k_lbfgs)
+    """Kernel attributes (dynamic LDS above 64 KB: k_leaf9 / k_node8 151 KB, LINV21's k_gemm, k_lauum_grad, k_lbfgs)
     are set once per device when a context is created (gprx_ctx_create, std::call_once), not by a
     process-wide flag at the first launch: four threads of a fresh process each create a context and
     at once run a B = 32 batch (the fused-leaf path) and its optimiser; every thread gets the serial
