@@ -438,12 +438,13 @@ def test_production_path_b32_full_size(gprx, ctx):
     b.close()
 
 
-@pytest.mark.parametrize("N", [512, 1024, 960])
+@pytest.mark.parametrize("N", [512, 1024, 960, 500, 1000])
 def test_production_path_n8_plan(gprx, ctx, N):
-    """B >= 32 at N = 512 (the root is an 8-tile node: its SYRK + TT launch runs the fixed plan of
-    gemm_body, node tiles read from K), N = 1024 (two 8-tile children: the bottom one reads the
-    updated tiles from S) and N = 960 (15 tiles: 7/8-tile nodes, the plan only where h = 4);
-    slots against the oracle and bit-identical across runs."""
+    """B >= 32 at N = 512 (the root is an 8-tile node: k_node8, its SYRK + TT on the fixed plan of
+    gemm_unit, node tiles read from K), N = 1024 (two 8-tile children: the bottom one reads the
+    updated tiles from S), N = 960 (15 tiles: 7/8-tile nodes, the plan only where h = 4), and the
+    padded sizes N = 500 and 1000 (the last tile part padding, inside k_node8); slots against the
+    oracle and bit-identical across runs."""
     from gprx import data
 
     B = 32
