@@ -1475,22 +1475,15 @@ __device__ __forceinline__ void gemm_tile(const DevBatch& db, const GemmGeom& g,
 #pragma unroll
           for (int q = 0; q < 4; ++q) tb[(16 * aa + lr) * TT_S + 16 * b + lk + 4 * q] = acc[2 * h + aa][b][q];
       __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_sched_barrier(0);
+      // all 16 reads in flight before the stores (one LDS round trip per round, not one per row
+      // pair); rows 32h + 2 r2 .. + 1: the pair's base in the resource (SGPRs), the lane's row
+      // parity and column pair in the VGPR offset (soffset 0: see buffer_store_f64x2)
+      double2 v[16];
 #pragma unroll
-      for (int r2 = 0; r2 < 16; ++r2) {
-        // rows 32h + 2 r2 .. + 1: the pair's base in the resource (SGPRs), the lane's row parity and
-        // column pair in the VGPR offset (soffset 0: see buffer_store_f64x2)
-        const double2 v = *(const double2*)(tb + (2 * r2 + hr) * TT_S + c2);
-        buffer_store_f64x2(buffer_rsrc(Mtt + (size_t)(32 * h + 2 * r2) * ld, 0x7ffffff0), vst, v.x, v.y);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      for (int r2 = 0; r2 < 16; ++r2) v[r2] = *(const double2*)(tb + (2 * r2 + hr) * TT_S + c2);
 #pragma unroll
-      for (int g = 0; g < 14; ++g) {
-        __builtin_amdgcn_sched_group_barrier(0x040, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x040, 2, 0);
-      __builtin_amdgcn_sched_barrier(0);
+      for (int r2 = 0; r2 < 16; ++r2)
+        buffer_store_f64x2(buffer_rsrc(Mtt + (size_t)(32 * h + 2 * r2) * ld, 0x7ffffff0), vst, v[r2].x, v[r2].y);
       __builtin_amdgcn_wave_barrier();
     }
     GTS(g, pass, 3);
