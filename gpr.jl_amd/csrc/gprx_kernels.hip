@@ -1421,10 +1421,9 @@ __device__ __forceinline__ void gemm_tile(const DevBatch& db, const GemmGeom& g,
         double v = 0.0;
 #pragma unroll
         for (int a = 0; a < QM; ++a) v = fma(acc[a][b][q], acc[a][b][q], v);
-        v += __shfl_xor(v, 1);
-        v += __shfl_xor(v, 2);
-        v += __shfl_xor(v, 4);
-        v += __shfl_xor(v, 8);
+        // the 16 lanes' sum by DPP (round 5: was four ds_bpermute exchanges per 32-bit half); the
+        // same partners and operand order as the xor-1/2/4/8 tree, so the same sums
+        v = row_sum16(v);
         if (lr == 0) db.var_part[((size_t)slot * db.nt + ti) * db.Mpad + tj * TS + 16 * b + lk + 4 * q] = v;
       }
     return;
