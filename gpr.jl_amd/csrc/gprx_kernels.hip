@@ -232,6 +232,22 @@ __device__ __forceinline__ double row_sum16(double v) {
   v += dpp_f64<0x140>(v);
   return v;
 }
+// v + v(lane ^ 16) and v + v(lane ^ 32) by gfx950's lane-swap instructions (VALU, no LDS round
+// trip as with ds_bpermute).  A swap of v with itself leaves v and its partner's value in every
+// lane, in one order or the other, so the sum of the two results is v + partner exactly (addition
+// commutes): the same values as v += __shfl_xor(v, 16 / 32) (scratch/permlane_check.hip).
+__device__ __forceinline__ double sum_xor16(double v) {
+  const long long b = __builtin_bit_cast(long long, v);
+  const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)b, (unsigned)b, false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
+  return __builtin_bit_cast(double, ((long long)hi[0] << 32) | lo[0]) + __builtin_bit_cast(double, ((long long)hi[1] << 32) | lo[1]);
+}
+__device__ __forceinline__ double sum_xor32(double v) {
+  const long long b = __builtin_bit_cast(long long, v);
+  const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)b, (unsigned)b, false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
+  return __builtin_bit_cast(double, ((long long)hi[0] << 32) | lo[0]) + __builtin_bit_cast(double, ((long long)hi[1] << 32) | lo[1]);
+}
 
 // lane m of each row of 16 lanes, broadcast to the row (DPP row_newbcast, gfx90a+; m folds to a
 // constant once the caller's loop is unrolled)
@@ -918,8 +934,7 @@ __device__ __forceinline__ void zp_acc4(const DevBatch& db, int slot, int ti, in
     for (int b = 0; b < QN; ++b)
 #pragma unroll
       for (int q = 0; q < 4; ++q) t = fma(acc[a][b][q], yv[b][q], t);
-    t += __shfl_xor(t, 16);
-    t += __shfl_xor(t, 32);
+    t = sum_xor32(sum_xor16(t));
     if (lk == 0) {
       z0[16 * a + lr] = sgn * t;
       z1[16 * a + lr] = 0.0;
@@ -1621,8 +1636,7 @@ __device__ __forceinline__ void zp_acc2(const DevBatch& db, int slot, int ti, in
     for (int b = 0; b < WN; ++b)
 #pragma unroll
       for (int q = 0; q < 4; ++q) t = fma(acc[a][b][q], yv[b][q], t);
-    t += __shfl_xor(t, 16);
-    t += __shfl_xor(t, 32);
+    t = sum_xor32(sum_xor16(t));
     if (lk == 0) z[16 * a + lr] = sgn * t;
   }
 }
@@ -1714,10 +1728,7 @@ __device__ __forceinline__ void gemm_tile_pair(const DevBatch& db, const GemmGeo
         double v = 0.0;
 #pragma unroll
         for (int a = 0; a < WM; ++a) v = fma(acc[a][b][q], acc[a][b][q], v);
-        v += __shfl_xor(v, 1);
-        v += __shfl_xor(v, 2);
-        v += __shfl_xor(v, 4);
-        v += __shfl_xor(v, 8);
+        v = row_sum16(v);  // the xor-1/2/4/8 tree's partners and order, by DPP
         if (lr == 0)
           db.var_part[((size_t)slot * db.nt + ti) * db.Mpad + tj * TS + 32 * wc + 16 * b + lk + 4 * q] = v;
       }
@@ -1909,8 +1920,7 @@ __device__ __forceinline__ void leaf_body(const DevBatch& db, int o, int n, int 
           double zt = 0.0;
 #pragma unroll
           for (int q = 0; q < 4; ++q) zt = fma(-acc[a][q], yv[q], zt);
-          zt += __shfl_xor(zt, 16);
-          zt += __shfl_xor(zt, 32);
+          zt = sum_xor32(sum_xor16(zt));
           if (lk == 0) zq[kz][w][16 * a + lr] = zt;
         }
       }
@@ -2721,8 +2731,8 @@ __global__ __launch_bounds__(NTHR) void k_alpha(DevBatch db, int phase) {
     for (int u = 0; u < 8; ++u) m[u] = mn[u];
   }
   double s0 = (acc[0].x + acc[1].x) + (acc[2].x + acc[3].x), s1 = (acc[0].y + acc[1].y) + (acc[2].y + acc[3].y);
-  s0 += __shfl_xor(s0, 32);  // the other column parity
-  s1 += __shfl_xor(s1, 32);
+  s0 = sum_xor32(s0);  // the other column parity
+  s1 = sum_xor32(s1);
   if (cp == 0) {
     part[pt][2 * rp] = s0;
     part[pt][2 * rp + 1] = s1;
@@ -3212,8 +3222,7 @@ __global__ __launch_bounds__(NTHR) void k_pred_cross(DevBatch db) {
   double* mup = sc + DMAX;  // [4 waves][64 test points]
 #pragma unroll
   for (int b = 0; b < 4; ++b) {
-    mp[b] += __shfl_xor(mp[b], 16);
-    mp[b] += __shfl_xor(mp[b], 32);
+    mp[b] = sum_xor32(sum_xor16(mp[b]));
   }
   if ((tid & 63) < 16) {
 #pragma unroll
