@@ -163,11 +163,38 @@ int dalloc(gprx_batch* b, T** p, size_t count) {
 
 void free_test(gprx_batch* b);
 
+// The GEMM cores, the Gram and the LINV21 store address their operands through buffer resources of
+// 0x7ffffff0 bytes from a tile origin, with 32-bit byte offsets (gprx_kernels.hip buffer_rsrc,
+// core_ptr): a K walk spans up to Npad columns of ld = Npad (the factorisation) or Npad rows of
+// ld = Mpad (the prediction variance's K*^T).  Beyond that range a load would silently read 0, so
+// such sizes are refused (N <= 16320 at M <= Npad).
+constexpr size_t BUF_LIMIT = 0x7ffffff0;
+bool sizes_addressable(size_t Npad, size_t Mpad) { return Npad * std::max(Npad, Mpad) * sizeof(double) < BUF_LIMIT; }
+size_t pad64(size_t n) { return (n + TS - 1) / TS * TS; }
+
+// Device bytes of a batch's test-point buffers (alloc_test) and of the whole batch
+// (gprx_batch_create); the same expressions as the allocations
+size_t test_bytes(size_t B, size_t d, size_t Npad, size_t Mpad) {
+  const size_t nt = Npad / TS;
+  return sizeof(double) * (B * Mpad * d + B * Npad * Mpad + 2 * B * nt * Mpad + 2 * B * Mpad);
+}
+size_t batch_bytes(size_t B, int d, size_t Npad, size_t Mpad) {
+  const size_t nt = Npad / TS, mat = Npad * Npad, xs = (size_t)(d | 1);
+  int ngu = 0, nimg = 0;
+  const size_t nlj = (size_t)std::max(gprx::lauum_plan((int)nt, d, &ngu, &nimg, nullptr), 0);
+  const size_t dbl = B * Npad * d + B * Npad * xs + B * Npad + 5 * B * mat + B * Npad + B * 2 * nt * Npad + B * Npad +
+                     B * (d + 4) + B * (d + 2) + B * nt + B * (size_t)ngu * (d + 2) + B * (d + 3);
+  const size_t ints = 2 * B + 2 * gprx::LU * nlj + B;
+  return dbl * sizeof(double) + ints * sizeof(int) + test_bytes(B, d, Npad, Mpad);
+}
+
 int alloc_test(gprx_batch* b, int M_max) {
   DevBatch& db = b->db;
   db.M = 0;
   db.Mpad = ((M_max + TS - 1) / TS) * TS;
   if (db.Mpad == 0) db.Mpad = TS;
+  if (!sizes_addressable(db.Npad, db.Mpad))
+    return set_err(b->ctx, GPRX_INVALID_ARGUMENT, "test points: Npad * max(Npad, Mpad) * 8 exceeds the 2 GiB buffer range");
   db.mt = db.Mpad / TS;
   const size_t B = db.B;
   int rc;
@@ -476,6 +503,9 @@ int gprx_batch_create(gprx_ctx* c, int B, int d, int N, int M_max, gprx_batch** 
   *out = nullptr;
   if (B < 1 || d < 1 || d > gprx::DMAX || N < 1 || M_max < 0)
     return set_err(c, GPRX_INVALID_ARGUMENT, "gprx_batch_create: need B>=1, 1<=d<=64, N>=1, M_max>=0");
+  if (!sizes_addressable(pad64(N), std::max<size_t>(pad64(M_max), TS)))
+    return set_err(c, GPRX_INVALID_ARGUMENT,
+                   "gprx_batch_create: Npad * max(Npad, Mpad) * 8 must stay below the 2 GiB buffer range (N <= 16320)");
   std::lock_guard<std::mutex> g(c->mu);
   if (hipSetDevice(c->device) != hipSuccess) return GPRX_DEVICE_ERROR;
   gprx_batch* b = new gprx_batch();
@@ -579,6 +609,26 @@ int gprx_batch_dims(const gprx_batch* b, int* B, int* d, int* N, int* M_max) {
   if (d) *d = b->db.d;
   if (N) *N = b->db.N;
   if (M_max) *M_max = b->db.Mpad;
+  return GPRX_OK;
+}
+
+int gprx_batch_bytes(int B, int d, int N, int M_max, uint64_t* bytes) {
+  if (bytes) *bytes = 0;
+  if (!bytes || B < 1 || d < 1 || d > gprx::DMAX || N < 1 || M_max < 0) return GPRX_INVALID_ARGUMENT;
+  const size_t Npad = pad64(N), Mpad = std::max<size_t>(pad64(M_max), TS);
+  if (!sizes_addressable(Npad, Mpad)) return GPRX_INVALID_ARGUMENT;
+  *bytes = batch_bytes((size_t)B, d, Npad, Mpad);
+  return GPRX_OK;
+}
+
+int gprx_ctx_mem_info(gprx_ctx* c, uint64_t* free_bytes, uint64_t* total_bytes) {
+  if (!c) return GPRX_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess) return GPRX_DEVICE_ERROR;
+  size_t f = 0, t = 0;
+  HIPCHK(c, hipMemGetInfo(&f, &t));
+  if (free_bytes) *free_bytes = f;
+  if (total_bytes) *total_bytes = t;
   return GPRX_OK;
 }
 
@@ -914,8 +964,13 @@ int gprx_batch_optimize(gprx_batch* b, const double* theta0, const gprx_opt_opti
   return GPRX_OK;
 }
 
-int gprx_batch_set_opt_trace(gprx_batch* b, double* trace, int max_rounds) {
+int gprx_batch_set_opt_trace(gprx_batch* b, double* trace, int max_rounds, int64_t capacity) {
   if (!b || max_rounds < 0 || (max_rounds > 0 && !trace)) return GPRX_INVALID_ARGUMENT;
+  const int64_t need = (int64_t)max_rounds * b->db.B * (2 * (int64_t)(b->db.d + 2) + 2);
+  if (max_rounds > 0 && capacity < need)
+    return set_err(b->ctx, GPRX_INVALID_ARGUMENT,
+                   "gprx_batch_set_opt_trace: capacity " + std::to_string(capacity) + " < max_rounds * B * (2(d+2)+2) = " +
+                       std::to_string(need) + " doubles");
   std::lock_guard<std::mutex> g(b->ctx->mu);
   b->opt_trace = max_rounds > 0 ? trace : nullptr;
   b->opt_trace_rounds = max_rounds;

@@ -64,6 +64,8 @@ SIGNATURES = {
     "gprx_ctx_set_option": (C.c_int, [_vp, C.c_int, C.c_int]),
     "gprx_ctx_kernel_stats": (C.c_int, [_vp, C.c_char_p, _dp, C.POINTER(C.c_int64), _dp, _dp]),
     "gprx_ctx_reset_stats": (C.c_int, [_vp]),
+    "gprx_ctx_mem_info": (C.c_int, [_vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    "gprx_batch_bytes": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_uint64)]),
     "gprx_batch_create": (C.c_int, [_vp, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(_vp)]),
     "gprx_batch_destroy": (None, [_vp]),
     "gprx_batch_set_train": (C.c_int, [_vp, _vp, C.c_int64, _vp, C.c_int64, C.c_int]),
@@ -74,7 +76,7 @@ SIGNATURES = {
     "gprx_batch_alpha": (C.c_int, [_vp, _dp]),
     "gprx_opt_defaults": (None, [C.POINTER(OptOptions)]),
     "gprx_batch_optimize": (C.c_int, [_vp, _dp, C.POINTER(OptOptions), _dp, _dp, _ip, _ip, _ip, _ip, _ip]),
-    "gprx_batch_set_opt_trace": (C.c_int, [_vp, _dp, C.c_int]),
+    "gprx_batch_set_opt_trace": (C.c_int, [_vp, _dp, C.c_int, C.c_int64]),
     "gprx_gp_create": (C.c_int, [_vp, _dp, C.c_int, C.c_int, _dp, C.POINTER(_vp)]),
     "gprx_gp_destroy": (None, [_vp]),
     "gprx_gp_lml": (C.c_int, [_vp, _dp, _dp]),

@@ -230,13 +230,13 @@ class GPBatch:
         tr = None
         if trace_rounds > 0:
             tr = np.full((int(trace_rounds), B, 2 * n + 2), np.nan)
-            L.check(L.lib.gprx_batch_set_opt_trace(self.h, L.dptr(tr), int(trace_rounds)), self.ctx.h)
+            L.check(L.lib.gprx_batch_set_opt_trace(self.h, L.dptr(tr), int(trace_rounds), tr.size), self.ctx.h)
         try:
             rc = L.lib.gprx_batch_optimize(self.h, L.dptr(theta0), C.byref(o), L.dptr(th), L.dptr(fmin), L.iptr(its),
                                            L.iptr(fc), L.iptr(gc), L.iptr(stp), C.byref(rounds))
         finally:
             if tr is not None:
-                L.lib.gprx_batch_set_opt_trace(self.h, None, 0)
+                L.lib.gprx_batch_set_opt_trace(self.h, None, 0, 0)
         self.last_opt_trace = tr[:max(0, min(int(rounds.value), tr.shape[0]))] if tr is not None else None
         if rc not in (L.OK, L.NOT_POSITIVE_DEFINITE, L.INVALID_ARGUMENT) or np.any(stp < 0):
             L.check(rc if rc != L.OK else L.DEVICE_ERROR, self.ctx.h)  # no search ran: no results

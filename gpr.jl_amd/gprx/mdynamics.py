@@ -136,10 +136,14 @@ def _gp_means(rb, feats) -> np.ndarray:
     """The GP means (k*^T alpha, no prior mean) of every slot of RankBatch rb at its trial's points:
     feats (n_local, d, M) -> (n_local, G, M), one batched device predict."""
     b = rb.batch
-    Xs = np.repeat(np.asarray(feats, dtype=np.float64), rb.G, axis=0)  # slot t*G + g: trial t's points
+    feats = np.asarray(feats, dtype=np.float64)
+    nd = getattr(rb, "n_dev", rb.n)
+    if nd > rb.n:  # a chunk padded to the group's launch geometry (shard.plan_chunks): copies of the last trial
+        feats = np.concatenate([feats, np.repeat(feats[-1:], nd - rb.n, axis=0)])
+    Xs = np.repeat(feats, rb.G, axis=0)  # slot t*G + g: trial t's points
     b.set_test(Xs)
     mu, _ = b.predict(variance=False)
-    return mu.reshape(rb.n, rb.G, -1)
+    return mu.reshape(nd, rb.G, -1)[: rb.n]
 
 
 def simulate(mech: str, cstates, steps: int, physics=None, ctx=None):

@@ -9,7 +9,9 @@ Here one process drives one GPU (torch.distributed; backend "nccl" = RCCL over x
   * trial-major round robin: whole trials go to ranks (`shard_trials`), and each rank evaluates
     ALL of its trials x G outputs as ONE device batch (`RankBatch`: B = local trials x G slots,
     built once, reused for every evaluation and optimiser round) -- the batching the bench
-    measures, instead of one small launch sequence per trial;
+    measures, instead of one small launch sequence per trial.  A rank whose group does not fit
+    the card (FB N=4096: 671 MB per slot) runs it as a few such batches one after another, sized
+    from the free HBM (`group_plan`), with results bit-identical to one batch;
   * no data moves between GPUs during a fit; trial inputs are generated (or loaded) on the rank
     that owns them;
   * when a single trial must be spread (G outputs over several GPUs, e.g. one P2 trial on 8
@@ -127,15 +129,94 @@ def _device(dev=None):
     return "cuda" if dist.get_backend() == "nccl" else "cpu"
 
 
+# ---- device-batch sizing: a rank's trials in batches that fit the card -----------------------
+# gprx_api.hip set_geometry: the recursion's leaf size and GEMM units switch at 32 slots, so a
+# batch under 32 slots rounds differently from one above.  Chunks of a group whose whole batch has
+# >= 32 slots are therefore padded to 32 (copies of their last trial, results discarded): every
+# chunk then runs the launch geometry the single batch would, and the results are bit-identical.
+GEOMETRY_SLOTS = 32
+
+
+def batch_bytes(B: int, d: int, N: int, M: int) -> int:
+    """Device bytes of GPBatch(B, d, N, M) (gprx_batch_bytes: host arithmetic, no GPU)."""
+    import ctypes as C
+
+    from . import _lib as L
+
+    out = C.c_uint64()
+    rc = L.lib.gprx_batch_bytes(int(B), int(d), int(N), int(M), C.byref(out))
+    if rc != L.OK:
+        raise L.GPRXError(rc, f"batch sizes B={B} d={d} N={N} M={M}")
+    return int(out.value)
+
+
+def default_budget(ctx) -> int:
+    """Device bytes a rank's batch may take: 90% of the free HBM less 1 GiB (the optimiser's
+    workspace, the rollouts' buffers and torch's own allocations come on top)."""
+    import ctypes as C
+
+    from . import _lib as L
+
+    free, total = C.c_uint64(), C.c_uint64()
+    L.check(L.lib.gprx_ctx_mem_info(ctx.h, C.byref(free), C.byref(total)), ctx.h)
+    return max(int(0.9 * free.value) - (1 << 30), 0)
+
+
+def plan_chunks(n_trials: int, G: int, slot_bytes: int, fixed_bytes: int, budget: int,
+                geometry_slots: int = GEOMETRY_SLOTS) -> list[tuple[int, int, int]]:
+    """Split n_trials trials of G slots into device batches of at most `budget` bytes
+    (slot_bytes per slot + fixed_bytes per batch).  Returns [(lo, hi, dev_trials)]: trials
+    [lo, hi) in one batch of dev_trials >= hi - lo trials (padding up to the 32-slot geometry
+    threshold when the whole group has >= 32 slots, so that chunked and single-batch results are
+    bit-identical).  Chunks are balanced (sizes differ by at most one trial).  A budget that cannot
+    hold one padded chunk raises MemoryError (the allocation would fail with GPRX_OUT_OF_MEMORY)."""
+    if n_trials <= 0:
+        return []
+    per_trial = slot_bytes * G
+    if fixed_bytes + n_trials * per_trial <= budget:
+        return [(0, n_trials, n_trials)]
+    pad = -(-geometry_slots // G) if n_trials * G >= geometry_slots else 1  # trials per chunk at least
+    fit = (budget - fixed_bytes) // per_trial if budget > fixed_bytes else 0
+    if fit < max(pad, 1):
+        raise MemoryError(f"gprx: a device batch of {max(pad, 1)} trial(s) x {G} outputs needs "
+                          f"{fixed_bytes + max(pad, 1) * per_trial} bytes, budget {budget}")
+    nch = -(-n_trials // fit)
+    base, extra = divmod(n_trials, nch)
+    out, lo = [], 0
+    for c in range(nch):
+        hi = lo + base + (1 if c < extra else 0)
+        out.append((lo, hi, max(hi - lo, pad)))
+        lo = hi
+    return out
+
+
+def group_plan(trials: Sequence[dict], ctx=None, budget: int | None = None) -> list[tuple[int, int, int]]:
+    """plan_chunks for a rank's trials (budget None: default_budget(ctx))."""
+    if not trials:
+        return []
+    d, N = np.asarray(trials[0]["X"]).shape
+    G = np.atleast_2d(trials[0]["Y"]).shape[0]
+    xs0 = trials[0].get("Xs")
+    M = 0 if xs0 is None else np.asarray(xs0).shape[1]
+    one, two = batch_bytes(1, d, N, M), batch_bytes(2, d, N, M)
+    if budget is None:
+        budget = default_budget(ctx)
+    return plan_chunks(len(trials), G, two - one, 2 * one - two, budget)
+
+
 # ---- the product evaluator: one device batch per rank ----------------------------------------
 class RankBatch:
-    """All of a rank's trials x G outputs as one GPBatch (B = n_local * G slots, slot t*G + g =
-    local trial t, output g), built once and reused.  Each trial's X / Xs is the slot's own input
+    """A rank's trials x G outputs as one GPBatch (B = n_local * G slots, slot t*G + g = local
+    trial t, output g), built once and reused.  Each trial's X / Xs is the slot's own input
     (trials differ), the G outputs of a trial share it.
 
-    trials: list of dicts X (d, N), Y (G, N) (targets minus prior mean), Xs (d, M) or None."""
+    trials: list of dicts X (d, N), Y (G, N) (targets minus prior mean), Xs (d, M) or None.
+    dev_trials > len(trials): the device batch holds that many trials, the extra ones copies of
+    the last (a chunk padded to the group's launch geometry, plan_chunks); they are evaluated and
+    their results dropped.  A group larger than the card runs as several RankBatches one after
+    another (group_plan; gprx.sweep.run_group, gpu_evaluator)."""
 
-    def __init__(self, trials: Sequence[dict], ctx=None, device: int | None = None):
+    def __init__(self, trials: Sequence[dict], ctx=None, device: int | None = None, dev_trials: int | None = None):
         from .batch import Context, GPBatch
 
         if ctx is None:
@@ -147,31 +228,43 @@ class RankBatch:
         if self.n == 0:
             self.batch = None
             return
+        self.n_dev = max(self.n, dev_trials or 0)
+        dev = list(trials) + [trials[-1]] * (self.n_dev - self.n)
         X0 = np.asarray(trials[0]["X"])
         self.d, self.N = X0.shape
         self.G = np.atleast_2d(trials[0]["Y"]).shape[0]
         xs0 = trials[0].get("Xs")
         self.M = 0 if xs0 is None else np.asarray(xs0).shape[1]
-        B = self.n * self.G
+        B = self.n_dev * self.G
         self.batch = GPBatch(B, self.d, self.N, self.M, ctx=ctx)
-        X = np.repeat(np.stack([np.asarray(t["X"], dtype=np.float64) for t in trials]), self.G, axis=0)
-        Y = np.concatenate([np.atleast_2d(np.asarray(t["Y"], dtype=np.float64)) for t in trials], axis=0)
+        X = np.repeat(np.stack([np.asarray(t["X"], dtype=np.float64) for t in dev]), self.G, axis=0)
+        Y = np.concatenate([np.atleast_2d(np.asarray(t["Y"], dtype=np.float64)) for t in dev], axis=0)
         self.batch.set_train(X, Y)
         if self.M:
-            Xs = np.repeat(np.stack([np.asarray(t["Xs"], dtype=np.float64) for t in trials]), self.G, axis=0)
+            Xs = np.repeat(np.stack([np.asarray(t["Xs"], dtype=np.float64) for t in dev]), self.G, axis=0)
             self.batch.set_test(Xs)
 
     def _shape(self, a):
-        return None if a is None else np.asarray(a).reshape((self.n, self.G) + np.asarray(a).shape[1:])
+        """Device rows (n_dev * G, ...) -> (n_local, G, ...), padding rows dropped."""
+        if a is None:
+            return None
+        a = np.asarray(a)
+        return a.reshape((self.n_dev, self.G) + a.shape[1:])[: self.n]
+
+    def _rows(self, theta):
+        """(n_local, G, d+2) -> (n_dev * G, d+2), the padding trials repeating the last trial's rows."""
+        th = np.asarray(theta, dtype=np.float64).reshape(self.n, self.G, -1)
+        if self.n_dev > self.n:
+            th = np.concatenate([th, np.repeat(th[-1:], self.n_dev - self.n, axis=0)])
+        return th.reshape(self.n_dev * self.G, -1)
 
     def evaluate(self, theta, grad: bool = True, predict: bool | None = None, variance: bool = True) -> dict:
         """theta (n_local, G, d+2) -> dict of (n_local, G, ...) arrays (mll, grad, mu, var, status,
         info)."""
         if self.batch is None:
             return {}
-        th = np.asarray(theta, dtype=np.float64).reshape(self.n * self.G, -1)
         pred = self.M > 0 if predict is None else predict
-        r = self.batch.run(th, grad=grad, predict=pred, variance=variance)
+        r = self.batch.run(self._rows(theta), grad=grad, predict=pred, variance=variance)
         return {k: self._shape(v) for k, v in r.items() if v is not None}
 
     def optimize(self, theta0, method=None, options=None) -> dict:
@@ -181,7 +274,7 @@ class RankBatch:
         experiment throws and the trial is dropped, core.jl:41-46), the others stay valid."""
         if self.batch is None:
             return {}
-        th0 = np.asarray(theta0, dtype=np.float64).reshape(self.n * self.G, -1)
+        th0 = self._rows(theta0)
         res, rounds = self.batch.optimize(th0, method, options, refit=False)
         thmin = np.stack([r.minimizer for r in res])
         ok = np.all(np.isfinite(thmin), axis=1)
@@ -206,17 +299,28 @@ class RankBatch:
             self.batch = None
 
 
-def gpu_evaluator(device: int | None = None, ctx=None):
-    """Evaluator for run_trials_sharded on this rank's GPU: one RankBatch over all local trials
-    (theta taken from each trial dict).  Callers that evaluate the same trials repeatedly (an
-    optimiser, a sweep) keep a RankBatch themselves and call its evaluate / optimize."""
+def gpu_evaluator(device: int | None = None, ctx=None, budget: int | None = None):
+    """Evaluator for run_trials_sharded on this rank's GPU: the local trials as RankBatches that
+    fit the card (group_plan; one batch when they fit), theta taken from each trial dict.  Callers
+    that evaluate the same trials repeatedly (an optimiser, a sweep) keep a RankBatch themselves
+    and call its evaluate / optimize."""
 
     def evaluate(trials):
-        rb = RankBatch(trials, ctx=ctx, device=device)
-        try:
-            return rb.evaluate(np.stack([np.atleast_2d(t["theta"]) for t in trials]))
-        finally:
-            rb.close()
+        c = ctx
+        if c is None:
+            import torch
+
+            from .batch import Context
+
+            c = Context(torch.cuda.current_device() if device is None else device)
+        parts = []
+        for lo, hi, nd in group_plan(trials, c, budget):
+            rb = RankBatch(trials[lo:hi], ctx=c, dev_trials=nd)
+            try:
+                parts.append(rb.evaluate(np.stack([np.atleast_2d(t["theta"]) for t in trials[lo:hi]])))
+            finally:
+                rb.close()
+        return {k: np.concatenate([p[k] for p in parts]) for k in parts[0]} if parts else {}
 
     return evaluate
 

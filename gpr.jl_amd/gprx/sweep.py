@@ -109,19 +109,45 @@ def local_trials(mech: str, N: int, variant: str, trial_ids, testsamples: int, c
 
 def run_group(mech: str, N: int, variant: str, trial_ids, ctx, testsamples: int = 100, simsteps: int = 20,
               max_evals: int | None = 30, time_limit: float = float("nan"), keep: bool = False,
-              trials: list | None = None) -> dict:
+              trials: list | None = None, budget: int | None = None) -> dict:
     """One (mechanism, N, variant) group for this rank's trials: device optimise of every GP,
     then the variant's evaluation.  Returns per-trial arrays (n_local, ...) and timings.
-    trials: prebuilt local_trials-shaped inputs (the hyper-parameter search's), else noise.jl's."""
-    from .optim import LBFGS, Options
-
+    trials: prebuilt local_trials-shaped inputs (the hyper-parameter search's), else noise.jl's.
+    The trials run as one device batch when they fit `budget` bytes (None: the free HBM,
+    shard.default_budget), else as several batches one after another (shard.group_plan), with
+    bit-identical results; keep=True (the batch returned for inspection) needs one batch."""
     if trials is None:
         trials = local_trials(mech, N, variant, trial_ids, testsamples, ctx)
     n = len(trials)
     if n == 0:
         return {}
+    plan = shard.group_plan(trials, ctx, budget)
+    if keep and len(plan) > 1:
+        raise ValueError(f"run_group(keep=True): the group needs {len(plan)} device batches")
+    parts = []
+    for lo, hi, nd in plan:
+        rb = shard.RankBatch(trials[lo:hi], ctx=ctx, dev_trials=nd)
+        part = _run_chunk(mech, variant, trials[lo:hi], rb, ctx, testsamples, simsteps, max_evals, time_limit)
+        if keep:
+            part.update(rb=rb, trials=trials)
+        else:
+            rb.close()
+        parts.append(part)
+    if len(parts) == 1:
+        return parts[0]
+    out = {k: np.concatenate([p[k] for p in parts]) for k in ("kstep_mse", "projectionerror", "failed", "mll", "theta",
+                                                              "status", "f_calls")}
+    out.update(rounds=sum(p["rounds"] for p in parts), t_opt=sum(p["t_opt"] for p in parts),
+               t_eval=sum(p["t_eval"] for p in parts), slots=sum(p["slots"] for p in parts), batches=len(parts))
+    return out
+
+
+def _run_chunk(mech, variant, trials, rb, ctx, testsamples, simsteps, max_evals, time_limit) -> dict:
+    """run_group's work for the trials of one device batch rb."""
+    from .optim import LBFGS, Options
+
+    n = len(trials)
     t0 = time.perf_counter()
-    rb = shard.RankBatch(trials, ctx=ctx)
     th0 = np.stack([t["theta"] for t in trials])
     opt = rb.optimize(th0, LBFGS(), Options(max_evals=max_evals, time_limit=time_limit))
     t_opt = time.perf_counter() - t0
@@ -193,14 +219,9 @@ def run_group(mech: str, N: int, variant: str, trial_ids, ctx, testsamples: int 
                 err[i] = data.position_mse(truth, pred)
                 failed[i] = False
     t_eval = time.perf_counter() - t1
-    out = dict(kstep_mse=err, projectionerror=perr, failed=failed, mll=opt["mll"], theta=opt["theta"], status=opt["status"],
-               f_calls=opt["f_calls"],
-               rounds=opt["rounds"], t_opt=t_opt, t_eval=t_eval, slots=n * G)
-    if keep:
-        out.update(rb=rb, trials=trials)
-    else:
-        rb.close()
-    return out
+    return dict(kstep_mse=err, projectionerror=perr, failed=failed, mll=opt["mll"], theta=opt["theta"],
+                status=opt["status"], f_calls=opt["f_calls"], rounds=opt["rounds"], t_opt=t_opt, t_eval=t_eval,
+                slots=n * G, batches=1)
 
 
 def run_vi_baseline(mech: str, trial_ids, testsamples: int = 100, simsteps: int = 20, ctx=None) -> dict:

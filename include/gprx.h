@@ -43,8 +43,11 @@ extern "C" {
 /* ABI versions:
  *   1  first release.
  *   2  gprx_opt_options.max_evals <= 0 means "no limit" (Optim's f_calls_limit = 0); under
- *      version 1, 0 was a real cap of zero evaluations.  No signature changed. */
-#define GPRX_ABI_VERSION 2
+ *      version 1, 0 was a real cap of zero evaluations.  No signature changed.
+ *   3  gprx_batch_set_opt_trace takes the trace buffer's capacity; new gprx_batch_bytes and
+ *      gprx_ctx_mem_info (device-batch chunking); gprx_batch_create / gprx_batch_set_test refuse
+ *      sizes beyond the kernels' 32-bit buffer addressing (Npad * max(Npad, Mpad) * 8 >= 2^31 - 16). */
+#define GPRX_ABI_VERSION 3
 
 /* status codes (mirrors the reference's failure modes) */
 #define GPRX_OK 0
@@ -105,10 +108,20 @@ int gprx_ctx_set_option(gprx_ctx* ctx, int option, int value);
 int gprx_ctx_kernel_stats(gprx_ctx* ctx, const char* kernel, double* total_ms, int64_t* launches,
                           double* algo_flops, double* algo_bytes);
 int gprx_ctx_reset_stats(gprx_ctx* ctx);
+/* free and total device memory of the context's device (hipMemGetInfo), for sizing batches      */
+int gprx_ctx_mem_info(gprx_ctx* ctx, uint64_t* free_bytes, uint64_t* total_bytes);
 
 /* ---- batch: B GP slots with equal (d, N); slot b has its own X_b, y_b, theta_b ------------ */
-/* M_max: maximum number of test points per slot (0 = no prediction).  d <= 64, N >= 1.        */
+/* M_max: maximum number of test points per slot (0 = no prediction).  d <= 64, N >= 1, and
+ * Npad * max(Npad, Mpad) * 8 < 2^31 - 16 (Npad, Mpad: N, M_max rounded up to 64; N <= 16320):
+ * the kernels address a matrix panel with 32-bit byte offsets.  Larger sizes: GPRX_INVALID_ARGUMENT. */
 int gprx_batch_create(gprx_ctx* ctx, int B, int d, int N, int M_max, gprx_batch** out);
+/* Device bytes gprx_batch_create(B, d, N, M_max) allocates (host arithmetic only, no device call;
+ * the optimiser's workspace, B * ((10 + 2m)(d+2) + 2m + 16) doubles, comes on top during
+ * gprx_batch_optimize).  GPRX_INVALID_ARGUMENT for sizes gprx_batch_create refuses.  Hosts split
+ * a rank's trials into device batches that fit the free memory with it (the reference's
+ * parallelrun holds no such limit: core.jl:27-67 runs every trial in host RAM).                 */
+int gprx_batch_bytes(int B, int d, int N, int M_max, uint64_t* bytes);
 void gprx_batch_destroy(gprx_batch* batch);
 /* X: d x N column-major per slot (column t = one CState), slot b at X + b*x_slot_stride
  *    (x_slot_stride = 0: all slots share one X, as the G outputs of one trial do);
@@ -191,10 +204,12 @@ int gprx_batch_optimize(gprx_batch* batch, const double* theta0, const gprx_opt_
 /* Diagnostics: record the optimiser's evaluations.  With a host buffer of max_rounds * B * (2(d+2)+2)
  * doubles registered, every later gprx_batch_optimize on this batch writes, for round r < max_rounds
  * and slot b, at trace[(r*B + b) * (2(d+2)+2)]: [active (1/0: evaluated in this round), theta(d+2)
- * as evaluated, mll, dmll(d+2) as answered]; rounds past the last are NaN.  The buffer must stay
- * valid while registered; max_rounds = 0 unregisters it.  (No reference counterpart: it makes the
- * device optimiser's evaluation sequence comparable with a host restatement's, gprx/optim.py.)  */
-int gprx_batch_set_opt_trace(gprx_batch* batch, double* trace, int max_rounds);
+ * as evaluated, mll, dmll(d+2) as answered]; rounds past the last are NaN.  capacity: the buffer's
+ * size in doubles; smaller than max_rounds * B * (2(d+2)+2) is GPRX_INVALID_ARGUMENT (nothing is
+ * registered).  The buffer must stay valid while registered; max_rounds = 0 unregisters it.  (No
+ * reference counterpart: it makes the device optimiser's evaluation sequence comparable with a
+ * host restatement's, gprx/optim.py.)                                                           */
+int gprx_batch_set_opt_trace(gprx_batch* batch, double* trace, int max_rounds, int64_t capacity);
 
 /* ---- single GP: the GPE surface, a batch of one ------------------------------------------- */
 int gprx_gp_create(gprx_ctx* ctx, const double* X, int d, int N, const double* y_minus_mean,

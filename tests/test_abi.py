@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version_and_status_strings():
-    assert L.lib.gprx_abi_version() == 2
+    assert L.lib.gprx_abi_version() == 3
     assert L.lib.gprx_status_string(1) == b"not positive definite"
 
 
@@ -142,3 +142,42 @@ def test_optimizer_options_are_validated_on_the_host():
                dict(method=LBFGS(linesearch=BackTracking(order=3))), dict(options=Options(g_abstol=math.nan))):
         with pytest.raises(ValueError):
             opt_options(**kw)
+
+
+def _bytes(B, d, N, M):
+    out = C.c_uint64()
+    rc = L.lib.gprx_batch_bytes(B, d, N, M, C.byref(out))
+    return rc, int(out.value)
+
+
+def test_batch_bytes_and_the_addressing_guard():
+    """gprx_batch_bytes (host arithmetic, no GPU): five Npad x Npad fp64 matrices per slot dominate,
+    linear in B; sizes past the kernels' 32-bit buffer offsets (Npad * max(Npad, Mpad) * 8 >= 2^31
+    - 16) are refused, as gprx_batch_create refuses them (a K walk past 2 GiB would read
+    zeros silently)."""
+    rc, b1 = _bytes(1, 26, 2048, 100)
+    assert rc == 0
+    rc, b2 = _bytes(2, 26, 2048, 100)
+    assert rc == 0
+    per = b2 - b1
+    assert 5 * 2048 * 2048 * 8 < per < 5.2 * 2048 * 2048 * 8
+    assert _bytes(240, 26, 2048, 100)[1] == b1 + 239 * per
+    # FB N=4096: 671 MB per slot (DESIGN.md section 3)
+    fb = _bytes(2, 52, 4096, 100)[1] - _bytes(1, 52, 4096, 100)[1]
+    assert 6.7e8 < fb < 6.9e8
+    # the limit: N = 16320 (Npad^2 * 8 = 2.13e9) is addressable, 16321 (Npad = 16384: 2^31) is not
+    assert _bytes(1, 13, 16320, 0)[0] == 0
+    assert _bytes(1, 13, 16321, 0)[0] == L.INVALID_ARGUMENT
+    # test points: N = 2048 allows Mpad * 2048 * 8 < 2^31 - 16, i.e. M <= 131008
+    assert _bytes(1, 13, 2048, 131008)[0] == 0
+    assert _bytes(1, 13, 2048, 131009)[0] == L.INVALID_ARGUMENT
+    for bad in ((0, 1, 1, 0), (1, 0, 1, 0), (1, 65, 1, 0), (1, 1, 0, 0), (1, 1, 1, -1)):
+        assert _bytes(*bad)[0] == L.INVALID_ARGUMENT
+    assert L.lib.gprx_batch_bytes(1, 1, 1, 0, None) == L.INVALID_ARGUMENT
+
+
+def test_opt_trace_capacity_is_checked_without_a_batch():
+    """gprx_batch_set_opt_trace(NULL, ...) is an argument error (the capacity check itself needs a
+    batch: tests/test_gpu.py::test_opt_trace_capacity_checked)."""
+    buf = np.zeros(8)
+    assert L.lib.gprx_batch_set_opt_trace(None, L.dptr(buf), 1, 8) == L.INVALID_ARGUMENT

@@ -544,6 +544,93 @@ def test_cp_all_26_outputs_n512(gprx, ctx):
     b.close()
 
 
+def test_cp_production_path_across_resident_rounds(gprx, ctx):
+    """BASELINE config CP on the path its throughput figures run through: 19 trials x all 26 CState
+    outputs = 494 slots (B >= 32: k_node8, one 8-wave workgroup per slot and CU, so the 256 CUs take
+    the slots in two resident rounds), CP inputs and the CP theta of config.json, each trial
+    jittered.  Slots from both rounds against the oracle at the adaptive CP bounds (cond(K) ~ 1e8),
+    and the whole batch bit-identical across two runs (CPnoise.jl:37-43)."""
+    from gprx import data
+
+    n_tr, G, N, M = 19, 26, 512, 64
+    trs = [data.make_trial("CP", N, M, seed=data.trial_seed("CP", 50 + t)) for t in range(n_tr)]
+    B = n_tr * G
+    X = np.stack([trs[s // G]["X"] for s in range(B)])
+    Y = np.stack([trs[s // G]["Xcurr"][s % G] for s in range(B)])
+    Xs = np.stack([trs[s // G]["Xs"] for s in range(B)])
+    th0 = data.theta0("CP", 512)
+    rng = np.random.default_rng(19)
+    T = np.repeat(np.stack([th0 + 0.05 * rng.standard_normal(th0.shape[0]) for _ in range(n_tr)]), G, axis=0)
+    b = gprx.GPBatch(B, 26, N, M, ctx=ctx)
+    b.set_train(X, Y)
+    b.set_test(Xs)
+    r1 = b.run(T, grad=True, predict=True)
+    r2 = b.run(T, grad=True, predict=True)
+    assert np.all(r1["status"] == 0)
+    for k in ("mll", "grad", "mu", "var"):
+        assert np.all(np.isfinite(r1[k]))
+        np.testing.assert_array_equal(r1[k], r2[k])
+    # first and last slots of each resident round of 256, and outputs of every kind: a constant
+    # coordinate (y = 0), positions, velocities, angular velocities
+    for s in (0, 8, 130, 255, 256, 300, 411, 493):
+        check_slot(r1, s, X[s], Y[s], T[s], Xs[s], ctx.dist_mode)
+    b.close()
+
+
+def test_batch_bytes_match_the_allocation(gprx, ctx):
+    """gprx_batch_bytes (the chunk planner's size) against the device memory a batch actually takes
+    (hipMemGetInfo before and after gprx_batch_create): equal up to the allocator's rounding."""
+    import ctypes as C
+
+    from gprx import _lib as L, shard
+
+    def free():
+        f, t = C.c_uint64(), C.c_uint64()
+        L.check(L.lib.gprx_ctx_mem_info(ctx.h, C.byref(f), C.byref(t)))
+        assert 0 < f.value <= t.value
+        return f.value
+
+    for B, d, N, M in ((8, 26, 2048, 100), (3, 52, 4096, 0)):
+        want = shard.batch_bytes(B, d, N, M)
+        f0 = free()
+        b = gprx.GPBatch(B, d, N, M, ctx=ctx)
+        used = f0 - free()
+        b.close()
+        assert abs(used - want) <= 0.01 * want + (64 << 20), (B, d, N, M, used, want)
+
+
+def test_opt_trace_capacity_checked(gprx, ctx, golden_dir):
+    """gprx_batch_set_opt_trace refuses a buffer smaller than max_rounds * B * (2(d+2)+2) doubles
+    (the write size was implied) and registers one that is large enough."""
+    from gprx import _lib as L
+
+    z = np.load(golden_dir / "p1_n50.npz")
+    b = gprx.GPBatch(2, z["X"].shape[0], z["X"].shape[1], 0, ctx=ctx)
+    n = z["X"].shape[0] + 2
+    need = 3 * 2 * (2 * n + 2)
+    buf = np.zeros(need)
+    assert L.lib.gprx_batch_set_opt_trace(b.h, L.dptr(buf), 3, need - 1) == L.INVALID_ARGUMENT
+    assert L.lib.gprx_batch_set_opt_trace(b.h, L.dptr(buf), 3, need) == L.OK
+    assert L.lib.gprx_batch_set_opt_trace(b.h, None, 0, 0) == L.OK
+    b.close()
+
+
+def test_batch_create_refuses_sizes_past_the_buffer_range(gprx, ctx):
+    """Npad * max(Npad, Mpad) * 8 >= 2^31 - 16 is refused before any allocation (the kernels'
+    32-bit buffer offsets would read zeros past it), for the training size and the test points."""
+    with pytest.raises(gprx.GPRXError) as e:
+        gprx.GPBatch(1, 4, 16321, 0, ctx=ctx)
+    assert e.value.status == 2
+    with pytest.raises(gprx.GPRXError) as e:
+        gprx.GPBatch(1, 4, 2048, 131009, ctx=ctx)
+    assert e.value.status == 2
+    b = gprx.GPBatch(1, 4, 2048, 64, ctx=ctx)
+    with pytest.raises(gprx.GPRXError) as e:  # growing the test capacity past the range
+        b.set_test(np.zeros((4, 131009)))
+    assert e.value.status == 2
+    b.close()
+
+
 def test_out_of_memory_batch_is_an_error_not_a_hang(gprx, ctx, golden_dir):
     """A batch larger than HBM fails with GPRX_OUT_OF_MEMORY (its partial allocations released
     under the context's own lock) and the context stays usable."""
@@ -972,12 +1059,14 @@ def test_reproducible_beside_another_gpu_process(gprx, ctx):
         b.close()
 
 
-def test_first_launches_from_concurrent_contexts_in_a_fresh_process(golden_dir):
-    """Kernel attributes (dynamic LDS above 64 KB: k_leaf9 / k_node8 151 KB, LINV21's k_gemm, k_lauum_grad, k_lbfgs)
-    are set once per device when a context is created (gprx_ctx_create, std::call_once), not by a
-    process-wide flag at the first launch: four threads of a fresh process each create a context and
-    at once run a B = 32 batch (the fused-leaf path) and its optimiser; every thread gets the serial
-    results."""
+@pytest.mark.parametrize("N", [256, 1024])
+def test_first_launches_from_concurrent_contexts_in_a_fresh_process(golden_dir, N):
+    """Kernel attributes (dynamic LDS above 64 KB: k_leaf9 / k_node8 151 KB, LINV21's k_gemm 67.6 KB,
+    k_lauum_grad, k_lbfgs) are set once per device when a context is created (gprx_ctx_create,
+    std::call_once), not by a process-wide flag at the first launch: four threads of a fresh process
+    each create a context and at once run a B = 32 batch and its optimiser; every thread gets the
+    serial results.  N = 256: the fused 4-tile leaf; N = 1024: two k_node8 nodes and the root's
+    LINV21 k_gemm, the launches whose LDS exceeds the 64 KB default."""
     import subprocess
     import sys
 
@@ -987,11 +1076,11 @@ sys.path.insert(0, sys.argv[1])
 import gprx
 from gprx import data
 from gprx.optim import LBFGS, Options
-B, N = 32, 256
+B, N = 32, int(sys.argv[2])
 trs = [data.make_trial("P2", N, 0, seed=data.trial_seed("P2", t)) for t in range(B // 6 + 1)]
 X = np.stack([trs[s // 6]["X"] for s in range(B)])
 Y = np.stack([trs[s // 6]["Y"][s % 6] for s in range(B)])
-T = np.tile(data.theta0("P2", 256), (B, 1))
+T = np.tile(data.theta0("P2", min(N, 2048)), (B, 1))
 go = threading.Barrier(4)
 out = [None] * 4
 def work(i):
@@ -1015,5 +1104,5 @@ print("ok")
     import pathlib
 
     pkg = str(pathlib.Path(__file__).resolve().parents[1] / "gpr.jl_amd")
-    r = subprocess.run([sys.executable, "-c", script, pkg], capture_output=True, text=True, timeout=240)
+    r = subprocess.run([sys.executable, "-c", script, pkg, str(N)], capture_output=True, text=True, timeout=240)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]

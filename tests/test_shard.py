@@ -5,6 +5,7 @@ import os
 import socket
 
 import numpy as np
+import pytest
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
@@ -111,3 +112,30 @@ def test_gloo_world3_with_an_idle_rank():
     """Fewer trials than ranks: rank 2 owns nothing and still takes part in every gather."""
     got = _run(3, 2)
     _check(got, 3, 2)
+
+
+def test_plan_chunks_budget_balance_and_geometry_padding():
+    """Device-batch chunking (shard.plan_chunks): one batch when the group fits; otherwise balanced
+    chunks under the budget, each padded to the 32-slot launch-geometry threshold when the whole
+    group is above it (so chunked results equal the single batch's bit for bit)."""
+    from gprx.shard import plan_chunks
+
+    slot, fixed = 1000, 50
+    assert plan_chunks(10, 6, slot, fixed, 10 * 6 * slot + fixed) == [(0, 10, 10)]
+    assert plan_chunks(0, 6, slot, fixed, 1) == []
+    p = plan_chunks(10, 6, slot, fixed, 6 * 6 * slot + fixed)  # 6 trials per batch fit -> 2 chunks of 5
+    assert p == [(0, 5, 6), (5, 10, 6)]  # 5 trials x 6 = 30 slots < 32: padded to 6 trials (36 slots)
+    p = plan_chunks(20, 6, slot, fixed, 7 * 6 * slot + fixed)  # 7 fit -> 3 chunks 7/7/6
+    assert p == [(0, 7, 7), (7, 14, 7), (14, 20, 6)]
+    assert all(nd * 6 >= 32 for _, _, nd in p)
+    # padding never exceeds the budget: 6 trials x 6 outputs must fit, else MemoryError
+    with pytest.raises(MemoryError):
+        plan_chunks(10, 6, slot, fixed, 5 * 6 * slot + fixed)
+    # FB-like: 100 trials x 12 outputs, 671 MB per slot, 250 GB budget -> 31 trials per batch fit
+    p = plan_chunks(100, 12, 671_000_000, 10_000, 250_000_000_000)
+    assert [h - l for l, h, _ in p] == [25, 25, 25, 25]
+    assert all(nd == h - l for l, h, nd in p)
+    assert p[0][0] == 0 and p[-1][1] == 100 and all(p[i][1] == p[i + 1][0] for i in range(len(p) - 1))
+    # a group under 32 slots is never padded (it already runs the small-batch geometry)
+    p = plan_chunks(5, 3, slot, fixed, 2 * 3 * slot + fixed)
+    assert [nd for _, _, nd in p] == [2, 2, 1] and [h - l for l, h, _ in p] == [2, 2, 1]

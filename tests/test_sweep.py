@@ -270,3 +270,56 @@ def test_meandynamics_variants_against_oracle(ctx, mech):
                     q_cur = q_cur + 0.01 * rates
                 np.testing.assert_allclose(fin[0, j], final_cstate(mech, q_cur), rtol=0, atol=1e-9)
         rb.close()
+
+
+@pytest.mark.parametrize("mech,N,variant,n_tr,fit", [("P2", 200, "max", 8, 6), ("CP", 100, "md_max", 12, 8),
+                                                     ("P2", 130, "min", 9, 4)])
+def test_chunked_group_equals_one_batch(ctx, mech, N, variant, n_tr, fit):
+    """A group whose trials do not fit the device budget runs as several device batches one after
+    another (shard.group_plan), with results bit-identical to one batch: the optimiser's minimisers,
+    f-call counts, LML, status and the rollout errors.  `fit` trials per batch fit the forced
+    budget; P2 max (6 outputs, 48 slots) and CP md_max (4 outputs, 48 slots) run two chunks padded
+    to the 32-slot launch geometry, P2 min (2 outputs, 18 slots) three unpadded chunks
+    (examples/hyperparameter.jl:43 runs 100 trials through one parallelrun, core.jl:27-67)."""
+    from gprx import shard, sweep
+
+    trials = sweep.local_trials(mech, N, variant, range(n_tr), 8, ctx)
+    G = np.atleast_2d(trials[0]["Y"]).shape[0]
+    d = trials[0]["X"].shape[0]
+    M = 0 if trials[0].get("Xs") is None else trials[0]["Xs"].shape[1]
+    one, two = shard.batch_bytes(1, d, N, M), shard.batch_bytes(2, d, N, M)
+    budget = (2 * one - two) + fit * G * (two - one)
+    plan = shard.group_plan(trials, ctx, budget)
+    assert len(plan) >= 2 and all(nd <= fit for _, _, nd in plan)
+    if n_tr * G >= 32:
+        assert all(nd * G >= 32 for _, _, nd in plan)
+    kw = dict(testsamples=8, simsteps=5, max_evals=12, trials=trials)
+    single = sweep.run_group(mech, N, variant, range(n_tr), ctx, **kw)
+    chunked = sweep.run_group(mech, N, variant, range(n_tr), ctx, budget=budget, **kw)
+    assert chunked["batches"] == len(plan) and single["batches"] == 1
+    for k in ("theta", "f_calls", "mll", "status", "kstep_mse", "projectionerror", "failed"):
+        np.testing.assert_array_equal(chunked[k], single[k], err_msg=k)
+    assert np.sum(single["status"] == 0) > 0
+    with pytest.raises(ValueError):
+        sweep.run_group(mech, N, variant, range(n_tr), ctx, budget=budget, keep=True, **kw)
+
+
+def test_gpu_evaluator_chunked_equals_one_batch(ctx):
+    """shard.gpu_evaluator (run_trials_sharded's product evaluator) with a budget that forces three
+    device batches: mll, gradient, mean and variance bit-identical to one batch."""
+    from gprx import data, shard
+
+    n_tr, N = 10, 256
+    trials = []
+    for t in range(n_tr):
+        tr = data.make_trial("P2", N, 12, seed=data.trial_seed("P2", 30 + t))
+        trials.append(dict(X=tr["X"], Y=tr["Y"], Xs=tr["Xs"], theta=np.tile(data.theta0("P2", N), (6, 1))))
+    one, two = shard.batch_bytes(1, 26, N, 12), shard.batch_bytes(2, 26, N, 12)
+    budget = (2 * one - two) + 6 * 6 * (two - one)
+    assert len(shard.group_plan(trials, ctx, budget)) == 2
+    a = shard.gpu_evaluator(ctx=ctx)(trials)
+    b = shard.gpu_evaluator(ctx=ctx, budget=budget)(trials)
+    assert set(a) == set(b) and {"mll", "grad", "mu", "var", "status"} <= set(a)
+    for k in a:
+        assert a[k].shape[:2] == (n_tr, 6)
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
