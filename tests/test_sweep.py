@@ -272,8 +272,8 @@ def test_meandynamics_variants_against_oracle(ctx, mech):
         rb.close()
 
 
-@pytest.mark.parametrize("mech,N,variant,n_tr,fit", [("P2", 200, "max", 8, 6), ("CP", 100, "md_max", 12, 8),
-                                                     ("P2", 130, "min", 9, 4)])
+@pytest.mark.parametrize("mech,N,variant,n_tr,fit", [("P2", 512, "max", 8, 6), ("CP", 128, "md_max", 12, 8),
+                                                     ("P2", 128, "min", 9, 4)])
 def test_chunked_group_equals_one_batch(ctx, mech, N, variant, n_tr, fit):
     """A group whose trials do not fit the device budget runs as several device batches one after
     another (shard.group_plan), with results bit-identical to one batch: the optimiser's minimisers,
