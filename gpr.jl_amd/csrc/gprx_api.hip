@@ -50,6 +50,7 @@ struct gprx_ctx {
   // recursion nodes of <= this many tiles use the 64 x 32 pair-unit GEMM; 0 = auto (set_geometry:
   // 4 for batches of >= 32 slots, every node below that) (GPRX_OPT_SMALL_N)
   int small_n = 0;
+  int node_waves = 0;  // GPRX_OPT_NODE_WAVES: 0 auto, 8 (k_node8), 4 (k_node8h)
   // replay each batch's launch sequence as a hipGraph (GPRX_OPT_GRAPHS).  Off by default: measured
   // equal to direct launches at B=1..192 (the launches are queued far ahead of the GPU).
   bool use_graphs = false;
@@ -76,7 +77,7 @@ struct gprx_batch {
   // captured evaluation graphs, one per (want_grad, want_pred); valid while the key matches
   hipGraphExec_t gexec[4] = {};
   DevBatch gkey[4];
-  int gkey_ctx[4][2] = {};
+  int gkey_ctx[4][3] = {};
   bool gvalid[4] = {};
 };
 
@@ -242,6 +243,7 @@ int copy_in(gprx_ctx* c, void* dst, const void* src, size_t bytes, int mem) {
 // Recursive Cholesky + inverse over tile range [o, o+n) (tile units), all slots in lock step.
 // upd: the node lies in the trailing block of an ancestor (its tiles were updated into S); the top
 // child inherits the parent's flag, the bottom child follows the parent's SYRK
+constexpr int NODE8H_MIN_SLOTS = 512;  // auto: k_node8h from two slots per CU on 256 CUs
 void factor_rec(gprx_ctx* c, hipStream_t st, const DevBatch& db, int o, int n, int upd) {
   const double T = TS, Bd = db.B;
   const int leaf = c->leaf_tiles > 0 ? c->leaf_tiles : (db.B >= 32 ? 4 : 1);
@@ -256,8 +258,10 @@ void factor_rec(gprx_ctx* c, hipStream_t st, const DevBatch& db, int o, int n, i
 #endif
   if (GPRX_NODE8 && n == 8 && leaf == 4 && db.B >= 32) {  // the whole node in one launch (k_node8)
     const double m = 4 * T;
-    timed(c, st, "node8", Bd * (4.0 * m * m * m / 3.0 + 4.0 * m * m * m), Bd * 8.0 * (16.0 * m * m + 6.5 * m * m),
-          [&] { gprx::launch_node8(db, o, upd, st); }, n);
+    // the 4-wave form (two slots per CU) when the slots outnumber the CUs by far; bit-identical
+    const bool four = c->node_waves == 4 || (c->node_waves == 0 && db.B >= NODE8H_MIN_SLOTS);
+    timed(c, st, four ? "node8h" : "node8", Bd * (4.0 * m * m * m / 3.0 + 4.0 * m * m * m),
+          Bd * 8.0 * (16.0 * m * m + 6.5 * m * m), [&] { gprx::launch_node8(db, o, upd, st, four); }, n);
     return;
   }
   if (n == 1) {
@@ -328,7 +332,8 @@ int run_graph(gprx_batch* b, bool want_grad, bool want_pred) {
   const DevBatch& db = b->db;
   const int gi = (want_grad ? 1 : 0) + (want_pred ? 2 : 0);
   const bool same = b->gvalid[gi] && memcmp(&b->gkey[gi], &db, sizeof(DevBatch)) == 0 &&
-                    b->gkey_ctx[gi][0] == c->leaf_tiles && b->gkey_ctx[gi][1] == c->small_n;
+                    b->gkey_ctx[gi][0] == c->leaf_tiles && b->gkey_ctx[gi][1] == c->small_n &&
+                    b->gkey_ctx[gi][2] == c->node_waves;
   if (!same) {
     if (b->gvalid[gi]) (void)hipGraphExecDestroy(b->gexec[gi]);
     b->gvalid[gi] = false;
@@ -347,6 +352,7 @@ int run_graph(gprx_batch* b, bool want_grad, bool want_pred) {
     memcpy(&b->gkey[gi], &db, sizeof(DevBatch));
     b->gkey_ctx[gi][0] = c->leaf_tiles;
     b->gkey_ctx[gi][1] = c->small_n;
+    b->gkey_ctx[gi][2] = c->node_waves;
     b->gvalid[gi] = true;
   }
   HIPCHK(c, hipGraphLaunch(b->gexec[gi], c->stream));
@@ -464,6 +470,10 @@ int gprx_ctx_set_option(gprx_ctx* c, int option, int value) {
       return GPRX_OK;
     case GPRX_OPT_GRAPHS:
       c->use_graphs = value != 0;
+      return GPRX_OK;
+    case GPRX_OPT_NODE_WAVES:
+      if (value != 0 && value != 4 && value != 8) return set_err(c, GPRX_INVALID_ARGUMENT, "node waves: 0 (auto), 4 or 8");
+      c->node_waves = value;
       return GPRX_OK;
   }
   return set_err(c, GPRX_INVALID_ARGUMENT, "unknown option");

@@ -230,7 +230,8 @@ void launch_center(const DevBatch& b, hipStream_t s);
 void launch_diag(const DevBatch& b, int jt, int upd, hipStream_t s);
 void launch_leaf(const DevBatch& b, int o, int n, int upd, hipStream_t s);
 // the first half of an 8-tile node (top leaf, TRSM, SYRK + TT) in one launch (k_node8; B >= 32)
-void launch_node8(const DevBatch& b, int o, int upd, hipStream_t s);  // a whole 8-tile node (k_node8)
+// four: the 4-wave form (k_node8h, two slots per CU; bit-identical results)
+void launch_node8(const DevBatch& b, int o, int upd, hipStream_t s, bool four = false);  // a whole 8-tile node (k_node8)
 // one launch; with g2.op != OP_NONE the units of g2 are appended to g's (independent ops)
 void launch_gemm(const DevBatch& b, const GemmGeom& g, hipStream_t s, const GemmGeom& g2 = GemmGeom{OP_NONE, 0, 0, 0});
 void launch_alpha(const DevBatch& b, hipStream_t s, int phase);

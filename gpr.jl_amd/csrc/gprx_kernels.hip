@@ -2679,6 +2679,441 @@ __global__ __launch_bounds__(2 * NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))
   gemm_unit<false, REV_A, false>(db, GemmGeom{OP_LINV21, o, 4, 8, upd}, none, slot, half, w, 2);
 }
 
+// ============================================================================================
+// k_node8h (round 6): the same 8-tile node on a 4-wave workgroup per slot in 68 KB of LDS, so two
+// slots share a CU (one wave of each per SIMD, 256 VGPRs each, as k_node8's two waves per SIMD).
+// k_node8 holds one slot per CU: its leaves are latency chains (the diagonal wave's factor, the
+// chain products, the task items' operand round trips) that leave the CU's MFMA pipes mostly idle,
+// and a launch of more slots than CUs (the CP batches, the sweeps' and searches' N = 512 .. 2048
+// groups) runs them round after round.  With two slots per CU one slot's leaf latency overlaps the
+// other's GEMM phases.  Every product, sum and store is k_node8's, in the same order: the results
+// are bit-identical (tests/test_gpu.py::test_node8_four_wave_form_bit_identical), so the launch
+// form never changes a result and the batch-size rule of set_geometry stays the only geometry one.
+// What changes against leaf9_body:
+//   * LDS: the tile image dT and ONE inverse image dX (leaf9: two, plus the chain's image Tc).  The
+//     chain writes L(k+1,k) into dT (tile k's image is dead once its inverse is in dX), reads it
+//     into registers, and writes tile k+1 over it after one more barrier.  The diagonal wave keeps
+//     the 16 x 16 block inverses Dinv_P in dT's unused strictly-upper blocks while it factors
+//     (diag_w1s), and writes the inverse into dX only after the previous step's readers of dX are
+//     done (xfree), so most of its tile still overlaps them.
+//   * the z partial quarters go to the slot's S buffer, in its unused upper tile (o, o + 3) (no
+//     kernel reads or writes S's strictly-upper off-diagonal tiles), and are summed in leaf9's
+//     order;
+//   * the chain takes its operands straight from L2 (no staging image), and its four quarters run
+//     on all four waves (the diagonal wave is idle during the chain);
+//   * the inverse items' Y(k, j) are parked in their own Linv destination instead of registers
+//     (any of the three task waves finishes any item; a counter orders park and reuse).
+// ============================================================================================
+struct Leaf4Sync {
+  int tk;         // task-wave barrier counter (3 per barrier)
+  int ch;         // chain barrier counter (4 per barrier)
+  int diag_done;  // diagonal tiles factored and inverted
+  int xfree;      // steps whose readers of dX are done
+  int crit;       // critical SYRK items done (monotonic)
+  int ypark;      // Y items parked (monotonic)
+};
+constexpr int L4_TW = 3;
+constexpr size_t leaf4_lds_bytes() { return (2 * TS * FS + 2 * TS) * sizeof(double) + sizeof(Leaf4Sync); }
+static_assert(leaf4_lds_bytes() >= linv21_lds_bytes(), "k_node8h: LINV21 transpose buffers exceed the leaf's LDS");
+static_assert(2 * leaf4_lds_bytes() <= 160 * 1024, "k_node8h: two workgroups per CU");
+// staging block of Dinv_P in the tile image's strictly-upper blocks: (row block, column block)
+__device__ __forceinline__ constexpr int l4_stage_r(int P) { return P == 3 ? 16 : 0; }
+__device__ __forceinline__ constexpr int l4_stage_c(int P) { return P == 3 ? 32 : 16 * (P + 1); }
+// w1_panel with Dinv_P read from its staging block (the same values as Xi's diagonal block)
+template <int P>
+__device__ __forceinline__ void w1_panel_s(double* T, int lr, int lk) {
+  constexpr int NT = 3 - P;
+  if constexpr (NT > 0) {
+    constexpr int c0 = 16 * P, R0 = l4_stage_r(P), C0 = l4_stage_c(P);
+    double bv[4], av[NT][4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      bv[s] = T[(C0 + 4 * s + lk) * FS + R0 + lr];
+#pragma unroll
+      for (int i = 0; i < NT; ++i) av[i][s] = T[(c0 + 4 * s + lk) * FS + 16 * (P + 1 + i) + lr];
+    }
+    d4 acc[NT];
+#pragma unroll
+    for (int i = 0; i < NT; ++i) acc[i] = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int i = 0; i < NT; ++i) acc[i] = mfma(av[i][s], bv[s], acc[i]);
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) T[(c0 + lr) * FS + 16 * (P + 1 + i) + lk + 4 * q] = acc[i][q];
+    wave_sync();
+    double pv[NT][4];
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) pv[i][s] = T[(c0 + 4 * s + lk) * FS + 16 * (P + 1 + i) + lr];
+    constexpr int NB = NT * (NT + 1) / 2;
+    d4 sacc[NB], old[NB];
+#pragma unroll
+    for (int b = 0, j = 0; j < NT; ++j)
+#pragma unroll
+      for (int i = j; i < NT; ++i, ++b) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) old[b][q] = T[(16 * (P + 1 + j) + lr) * FS + 16 * (P + 1 + i) + lk + 4 * q];
+        sacc[b] = (d4){0.0, 0.0, 0.0, 0.0};
+      }
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int b = 0, j = 0; j < NT; ++j)
+#pragma unroll
+        for (int i = j; i < NT; ++i, ++b) sacc[b] = mfma(pv[i][s], pv[j][s], sacc[b]);
+#pragma unroll
+    for (int b = 0, j = 0; j < NT; ++j)
+#pragma unroll
+      for (int i = j; i < NT; ++i, ++b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) T[(16 * (P + 1 + j) + lr) * FS + 16 * (P + 1 + i) + lk + 4 * q] = old[b][q] - sacc[b][q];
+    wave_sync();
+  }
+}
+// diag_w1 with the block inverses staged in T; before_inverse() runs between the factor and the
+// inverse (the wait for dX's readers), then the staged blocks go to Xi and the off-diagonal inverse
+// blocks follow as in diag_w1
+template <class F>
+__device__ __forceinline__ void diag_w1s(const DevBatch& db, int slot, int jt, double* T, double* Xi, double* ldiag,
+                                         F&& before_inverse) {
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  int fail = -1;
+  for (int P = 0; P < 4; ++P) {
+    const int c0 = 16 * P;
+    double a[16], y[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      a[k] = T[(c0 + k) * FS + c0 + lr];
+      y[k] = (k == lr) ? 1.0 : 0.0;
+    }
+    double d = T[(c0 + lr) * FS + c0 + lr], pv = 1.0;
+    int fl = -1;
+    fact_step<0>(a, y, d, pv, lr, fl);
+    fl = __builtin_amdgcn_readfirstlane(fl);
+    if (fail < 0 && fl >= 0) fail = c0 + fl;
+    {
+      double sl, rl;
+      sqrt_rsqrt(pv, sl, rl);
+      fact_scale<0>(a, y, rl, sl, lr);
+    }
+    if (l < 16) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) T[(c0 + k) * FS + c0 + l] = (k <= l) ? a[k] : 0.0;
+      ldiag[c0 + l] = a[l];
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (l < 16) {
+      const int R0 = P == 3 ? 16 : 0, C0 = P == 3 ? 32 : 16 * (P + 1);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) T[(C0 + l) * FS + R0 + r] = y[r];
+    }
+    wave_sync();
+    switch (P) {
+      case 0: w1_panel_s<0>(T, lr, lk); break;
+      case 1: w1_panel_s<1>(T, lr, lk); break;
+      case 2: w1_panel_s<2>(T, lr, lk); break;
+      default: break;
+    }
+  }
+  before_inverse();
+#pragma unroll
+  for (int P = 0; P < 4; ++P) {
+    const int R0 = P == 3 ? 16 : 0, C0 = P == 3 ? 32 : 16 * (P + 1);
+#pragma unroll
+    for (int e = l; e < 256; e += 64) {
+      const int r = e & 15, c = e >> 4;
+      Xi[(16 * P + c) * FS + 16 * P + r] = T[(C0 + c) * FS + R0 + r];
+    }
+  }
+  wave_sync();
+  w1_inverse<1>(T, Xi, lr, lk);
+  w1_inverse<2>(T, Xi, lr, lk);
+  w1_inverse<3>(T, Xi, lr, lk);
+  if (fail >= 0 && l == 0 && db.status[slot] == 0) {
+    db.status[slot] = 1;
+    db.info[slot] = jt * TS + fail + 1;
+  }
+}
+// rot: the wave roles rotate by rot (0 or 2): the diagonal wave, the VALU-bound routine, is wave
+// rot, so that two workgroups sharing a CU can put their diagonal waves on different SIMDs
+__device__ __forceinline__ void leaf4_body(const DevBatch& db, int o, int upd, int rot) {
+  constexpr int n = 4;
+  extern __shared__ __attribute__((aligned(16))) double l4a[];
+  double* dT = l4a;                    // the tile image; the chain's L(k+1,k); Dinv staging
+  double* dX = dT + TS * FS;           // the inverse image Linv_kk
+  double* ldiag = dX + TS * FS;        // [2][64]: the diagonal of L_kk (log-determinant)
+  Leaf4Sync& sy = *(Leaf4Sync*)(ldiag + 2 * TS);
+  const int slot = blockIdx.x;
+  const int wave = (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) + rot) & 3;  // this wave's role
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  const size_t ld = db.ld, so = (size_t)slot * db.mat;
+  const int ldi = (int)ld;
+  const int lo = lk * ldi + lr, lo2 = lr * ldi + lk, llo = lk * FS + lr;
+  double* S = db.S + so;
+  const double* K0 = (upd ? db.S : db.K) + so;
+  double* Lw = db.Lw + so;
+  double* Li = db.Linv + so;
+  double* Mt = db.Mt + so;
+  const double* Y = db.Y + (size_t)slot * db.Npad;
+  // z partial quarters in S's upper tile (o, o + 3): column 4 kz + c (off-diagonal tile kz), 24 +
+  // 4 t + c (diagonal tile t), row r
+  double* zg = S + (size_t)(o + 3) * TS * ld + o * TS;
+  {  // tile o into the image
+    const double* A = K0 + (size_t)o * TS * ld + o * TS;
+    double v[TS * TS / NTHR];
+#pragma unroll
+    for (int k = 0; k < TS * TS / NTHR; ++k) {
+      const int e = threadIdx.x + k * NTHR, r = e & 63, c = e >> 6;
+      v[k] = (r >= c) ? A[(size_t)c * ld + r] : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < TS * TS / NTHR; ++k) {
+      const int e = threadIdx.x + k * NTHR, r = e & 63, c = e >> 6;
+      dT[c * FS + r] = v[k];
+    }
+    if (threadIdx.x == 0) {
+      sy.tk = 0;
+      sy.ch = 0;
+      sy.diag_done = 0;
+      sy.xfree = 0;
+      sy.crit = 0;
+      sy.ypark = 0;
+    }
+  }
+  __syncthreads();
+  const int cq = 16 * wave;  // this wave's chain quarter
+  int cgen = 0;
+  // the chain of step k on all four waves: L(k1, kk) rows cq.. = A(k1, kk) Linv_kk^T, then tile
+  // k1 = A(k1, k1) - L L^T into dT (leaf9_body's products, operands from L2)
+  auto chain = [&](int k, int ncrit) {
+    const double* Kc = k > 0 ? S : K0;
+    const int kk = o + k, k1 = kk + 1;
+    lds_wait_ge(&sy.crit, ncrit, db, slot);  // S(k1, kk), S(k1, k1) of the previous step
+    d4 cp[QM];
+#pragma unroll
+    for (int a = 0; a < QM; ++a)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) cp[a][q] = -Kc[(k1 * TS + 16 * a + 4 * q) * ldi + k1 * TS + cq + lo];
+    double bp[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) bp[s] = Kc[(kk * TS + 4 * s) * ldi + k1 * TS + cq + lo];
+    d4 u[QM];
+    acc_zero4(u);
+    lmma_tri(u, dX, bp);
+#pragma unroll
+    for (int a = 0; a < QM; ++a)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        Lw[(kk * TS + 16 * a + 4 * q) * ldi + k1 * TS + cq + lo] = u[a][q];
+        dT[(16 * a + 4 * q) * FS + cq + llo] = u[a][q];
+      }
+    ctr_barrier(&sy.ch, cgen, 4, db, slot);
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const double b = u[s >> 2][s & 3];
+#pragma unroll
+      for (int a = 0; a < QM; ++a) cp[a] = mfma(dT[4 * s * FS + 16 * a + llo], b, cp[a]);
+    }
+    ctr_barrier(&sy.ch, cgen, 4, db, slot);  // every quarter's reads of L(k1, kk) done
+#pragma unroll
+    for (int a = 0; a < QM; ++a)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int x = 16 * a + lk + 4 * q;
+        dT[(16 * a + 4 * q) * FS + cq + llo] = (cq + lr >= x) ? -cp[a][q] : 0.0;
+      }
+    ctr_barrier(&sy.ch, cgen, 4, db, slot);  // tile k1 in dT
+  };
+  if (wave == 0) {  // ---- the diagonal tiles, and chain quarter 0
+    int ncrit = 0;
+    for (int k = 0; k < n; ++k) {
+      diag_w1s(db, slot, o + k, dT, dX, ldiag + (k & 1) * TS, [&] { lds_wait_ge(&sy.xfree, k, db, slot); });
+      lds_publish(&sy.diag_done, k + 1);
+      if (k == n - 1) break;
+      chain(k, ncrit);
+      ncrit += 4 * l9_crit_tiles(n - 1 - k);
+    }
+  } else {  // ---- the task waves 1..3: chain quarters 1..3 and every tile item
+    const int tw = wave - 1;
+    int gen = 0, ncrit = 0;
+    for (int k = 0; k < n; ++k) {
+      const int kk = o + k;
+      const double* Kc = k > 0 ? S : K0;
+      lds_wait_gt(&sy.diag_done, k, db, slot);
+      if (k < n - 1) chain(k, ncrit);
+      // ---- phase A: X(k, j) = -Linv_kk Y(k, j) (Y parked in the item's Linv destination), the
+      //      diagonal tile's stores (4 column quarters), the TRSM rows of column k
+      {
+        const int nx = 4 * k, nt1 = n - 2 - k > 0 ? n - 2 - k : 0, na = nx + 4 + 4 * nt1;
+        bool waited_y = false, waited_c = false;
+        for (int e = tw; e < na; e += L4_TW) {
+          if (e < nx) {
+            if (!waited_y) {  // Y(k, .) of the previous step's phase B
+              lds_wait_ge(&sy.ypark, 2 * k * (k + 1), db, slot);
+              waited_y = true;
+            }
+            const int j = e >> 2, c = e & 3, tj = o + j, xq = 16 * c;
+            double b[16];
+#pragma unroll
+            for (int s = 0; s < 16; ++s) b[s] = Li[(tj * TS + xq) * ldi + kk * TS + 16 * (s >> 2) + 4 * (s & 3) + lo2];
+            d4 x[QM];
+            acc_zero4(x);
+            lmma_tri(x, dX, b);
+            const double yv = Y[tj * TS + xq + lr];
+#pragma unroll
+            for (int a = 0; a < QM; ++a) {
+              double zt[4];
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                const double v = -x[a][q];
+                Li[(tj * TS + xq) * ldi + kk * TS + 16 * a + 4 * q + lo2] = v;
+                Mt[(kk * TS + 16 * a + 4 * q) * ldi + tj * TS + xq + lo] = v;
+                zt[q] = row_sum16(v * yv);
+              }
+              if (lr == 0) {
+                const int kz = k * (k - 1) / 2 + j;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) zg[(size_t)(4 * kz + c) * ld + 16 * a + lk + 4 * q] = zt[q];
+              }
+            }
+          } else if (e < nx + 4) {  // columns xq.. of the diagonal tile: Linv, Mt = Linv^T, z partial
+            const int c = e - nx, xq = 16 * c;
+            double* Lc = Li + (size_t)kk * TS * ld + kk * TS;
+            double* Mc = Mt + (size_t)kk * TS * ld + kk * TS;
+            const int r = l;
+            double t = 0.0;
+#pragma unroll 4
+            for (int cc = xq; cc < xq + 16; ++cc) {
+              const double xv = r >= cc ? dX[cc * FS + r] : 0.0;
+              Lc[(size_t)cc * ld + r] = xv;
+              Mc[(size_t)cc * ld + r] = (cc >= r) ? dX[r * FS + cc] : 0.0;
+              t = fma(xv, Y[kk * TS + cc], t);
+            }
+            zg[(size_t)(24 + 4 * k + c) * ld + r] = t;
+            if (c == 0) {
+              const double lsum = wave_sum(log(ldiag[(k & 1) * TS + l]));
+              if (l == 0) db.logdet_part[(size_t)slot * db.nt + kk] = lsum;
+            }
+          } else {  // T(ti, kk) rows xq..
+            if (!waited_c) {  // S(ti, kk): the previous step's critical items
+              lds_wait_ge(&sy.crit, ncrit, db, slot);
+              waited_c = true;
+            }
+            const int f = e - nx - 4, c = f & 3, xq = 16 * c, ti = kk + 2 + (f >> 2);
+            double b[16];
+#pragma unroll
+            for (int s = 0; s < 16; ++s) b[s] = Kc[(kk * TS + 4 * s) * ldi + ti * TS + xq + lo];
+            d4 u[QM];
+            acc_zero4(u);
+            lmma_tri(u, dX, b);
+#pragma unroll
+            for (int a = 0; a < QM; ++a)
+#pragma unroll
+              for (int q = 0; q < 4; ++q) Lw[(kk * TS + 16 * a + 4 * q) * ldi + ti * TS + xq + lo] = u[a][q];
+          }
+        }
+      }
+      ctr_barrier(&sy.tk, gen, L4_TW, db, slot);
+      if (wave == 1) lds_publish(&sy.xfree, k + 1);  // every reader of dX in step k is past the barrier
+      if (k == n - 1) break;
+      // ---- phase B: the critical SYRK rows (counted), Y(k+1, j) (parked, counted), the other
+      //      SYRK rows; round robin over the task waves in that order
+      {
+        const int k1 = kk + 1;
+        const int ny = 4 * (k + 1);
+        const int m = n - 1 - k;
+        const int nsy = m * (m + 1) / 2 - 1;
+        const int nc4 = 4 * l9_crit_tiles(m);
+        for (int g = tw; g < ny + 4 * nsy; g += L4_TW) {
+          if (g >= nc4 && g < nc4 + ny) {  // Y(k1, tj)[:, xq..], parked at Linv(k1, tj)[:, xq..]
+            const int e = g - nc4, j = e >> 2, c = e & 3, tj = o + j, xq = 16 * c;
+            d4 yh[QM];
+            acc_zero4(yh);
+            mma_rd(yh, Lw + (size_t)(tj * TS + xq) * ld + k1 * TS, ld, Mt + (size_t)(tj * TS + xq) * ld + tj * TS + xq, ld,
+                   (k1 - tj) * TS - xq);
+#pragma unroll
+            for (int a = 0; a < QM; ++a)
+#pragma unroll
+              for (int q = 0; q < 4; ++q) Li[(tj * TS + xq) * ldi + k1 * TS + 16 * a + 4 * q + lo2] = yh[a][q];
+            lds_count(&sy.ypark);
+            continue;
+          }
+          const int e = g < nc4 ? g : g - ny;  // SYRK row item e
+          const int c = e & 3, xq = 16 * c;
+          int u = (e >> 2) + 1, cc = 0;
+          while (u >= m - cc) {
+            u -= m - cc;
+            ++cc;
+          }
+          const int tj = k1 + cc, ti = tj + u;
+          d4 acc[QM];
+#pragma unroll
+          for (int a = 0; a < QM; ++a)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[a][q] = -Kc[(tj * TS + 16 * a + 4 * q) * ldi + ti * TS + xq + lo];
+          mma_rd(acc, Lw + (size_t)kk * TS * ld + tj * TS, ld, Lw + (size_t)kk * TS * ld + ti * TS + xq, ld, TS);
+#pragma unroll
+          for (int a = 0; a < QM; ++a)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) S[(tj * TS + 16 * a + 4 * q) * ldi + ti * TS + xq + lo] = -acc[a][q];
+          if (g < nc4) lds_count(&sy.crit);
+        }
+        ncrit += nc4;
+      }
+    }
+  }
+  __syncthreads();
+  // z partials: the quarters summed in quarter order (leaf9_body's sums)
+  for (int e = threadIdx.x; e < (n + 6) * TS; e += NTHR) {
+    const int t = e >> 6, r = e & 63;
+    int ti, tj;
+    double v;
+    if (t < n) {
+      ti = tj = o + t;
+      const double* q0 = zg + (size_t)(24 + 4 * t) * ld + r;
+      v = ((q0[0] + q0[ld]) + q0[2 * ld]) + q0[3 * ld];
+    } else {
+      const int kz = t - n;
+      int k = 1;
+      while (k * (k + 1) / 2 <= kz) ++k;
+      ti = o + k;
+      tj = o + (kz - k * (k - 1) / 2);
+      const double* q0 = zg + (size_t)(4 * kz) * ld + r;
+      v = ((q0[0] + q0[ld]) + q0[2 * ld]) + q0[3 * ld];
+    }
+    zp_row(db, slot, 2 * tj)[ti * TS + r] = v;
+    zp_row(db, slot, 2 * tj + 1)[ti * TS + r] = 0.0;
+  }
+}
+__global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_node8h(DevBatch db, int o, int upd) {
+  const int slot = blockIdx.x;
+  if (slot >= db.B || !slot_active(db, slot)) return;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const GemmGeom none{OP_NONE, 0, 0, 0};
+#ifndef GPRX_N8H_ROT
+#define GPRX_N8H_ROT 1
+#endif
+  // workgroups b and b + 256 tend to share a CU (256 CUs filled in block order)
+  const int rot = GPRX_N8H_ROT == 1 ? ((blockIdx.x >> 8) & 1) * 2 : 0;
+  leaf4_body(db, o, upd, rot);
+  __syncthreads();
+#pragma unroll 1
+  for (int u = 0; u < 2; ++u) gemm_unit<false, REV_B, false>(db, GemmGeom{OP_TRSM, o, 4, 8, upd}, none, slot, u, wave, 2);
+  __syncthreads();
+#pragma unroll 1
+  for (int u = 0; u < 2; ++u)
+    gemm_unit<false, TRI_A_FIRST, false>(db, GemmGeom{OP_SYRK, o, 4, 8, upd}, GemmGeom{OP_TT, o, 4, 8, upd}, slot, u, wave, 2);
+  __syncthreads();
+  leaf4_body(db, o + 4, 1, rot);
+  __syncthreads();
+#pragma unroll 1
+  for (int u = 0; u < 2; ++u) gemm_unit<false, REV_A, false>(db, GemmGeom{OP_LINV21, o, 4, 8, upd}, none, slot, u, wave, 2);
+}
+
 
 
 // ============================================================================================
@@ -3373,6 +3808,7 @@ void set_kernel_attributes() {
     (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)cross_lds(DMAX));
   for (const void* f : {(const void*)k_leaf9, (const void*)k_node8})
     (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)leaf9_lds_bytes());
+  (void)hipFuncSetAttribute((const void*)k_node8h, hipFuncAttributeMaxDynamicSharedMemorySize, (int)leaf4_lds_bytes());
   for (const void* f : {(const void*)k_gemm<REV_A>, (const void*)k_gemm<REV_B>, (const void*)k_gemm<TRI_A_FIRST>})
     (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)linv21_lds_bytes());
   set_lbfgs_attributes();
@@ -3398,8 +3834,9 @@ void launch_leaf(const DevBatch& b, int o, int n, int upd, hipStream_t s) {
   }
   hipLaunchKernelGGL(k_leaf, dim3(b.B), dim3(NTHR), 0, s, b, o, n, upd);
 }
-void launch_node8(const DevBatch& b, int o, int upd, hipStream_t s) {
-  hipLaunchKernelGGL(k_node8, dim3(b.B), dim3(2 * NTHR), leaf9_lds_bytes(), s, b, o, upd);
+void launch_node8(const DevBatch& b, int o, int upd, hipStream_t s, bool four) {
+  if (four) hipLaunchKernelGGL(k_node8h, dim3(b.B), dim3(NTHR), leaf4_lds_bytes(), s, b, o, upd);
+  else hipLaunchKernelGGL(k_node8, dim3(b.B), dim3(2 * NTHR), leaf9_lds_bytes(), s, b, o, upd);
 }
 void launch_gemm(const DevBatch& b, const GemmGeom& g, hipStream_t s, const GemmGeom& g2) {
   if (g.op != OP_PREDVAR && g.n <= b.small_n) {  // small node: pair units, 64 x 32 waves

@@ -31,6 +31,7 @@ MEM_DEVICE = 1
 OPT_LEAF_TILES = 1
 OPT_SMALL_N = 2
 OPT_GRAPHS = 3
+OPT_NODE_WAVES = 4
 
 STOP_NAMES = {0: "iterations", 1: "g_tol", 2: "x_tol", 3: "f_tol", 4: "linesearch", 5: "max_evals", 6: "time_limit",
               7: "nan_gradient"}

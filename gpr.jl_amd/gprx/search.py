@@ -158,6 +158,7 @@ def run(experiments=EXPERIMENTS, sizes=SIZES, n_trials: int = 100, testsamples: 
             d = 13 * data.NBODIES[mech] if coords == "MAX" else 2 * len(data.MIN_COORDS[mech])
             r = run_search_group(exp, N, mine, ctx, testsamples, simsteps, max_evals, time_limit)
             n = len(mine)
+            nb = int(r.get("batches", 1 if r else 0))
             local = {"kstep_mse": r.get("kstep_mse", np.zeros(0)),
                      "failed": r.get("failed", np.zeros(0, dtype=bool)).astype(np.float64),
                      "params": r.get("params", np.zeros((0, d + 1))),
@@ -177,6 +178,7 @@ def run(experiments=EXPERIMENTS, sizes=SIZES, n_trials: int = 100, testsamples: 
                                           "kstep_mse": [float(v) for v in g["kstep_mse"][keep, 0]],
                                           "dropped": int((~keep).sum())}
                 timing[key] = {"seconds_max_rank": float(np.max(g["t"][:, 0])) if n_trials else 0.0,
+                               "device_batches_rank0": nb,
                                "gp_fits": n_trials * (len(data.VW_INDICES[mech]) if coords == "MAX"
                                                       else len(data.MIN_COORDS[mech]))}
                 if log:

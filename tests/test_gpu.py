@@ -410,6 +410,46 @@ def test_fused_node_failure_isolated(gprx, ctx):
     b.close()
 
 
+@pytest.mark.parametrize("N,B,mech", [(512, 64, "CP"), (1024, 40, "P2"), (500, 36, "P2"), (2048, 32, "P2")])
+def test_node8_four_wave_form_bit_identical(gprx, ctx, N, B, mech):
+    """The 4-wave form of the whole-8-tile-node kernel (k_node8h: two slots per CU, one inverse
+    image, the chain on all four waves, parked inverse items, z partials in S's free upper tile)
+    gives k_node8's results bit for bit: LML, gradient, mean, variance, status and failing pivot,
+    including a failing slot (NaN point: pivot 101 in the top leaf, 301 in the bottom leaf) and the
+    nodes an ancestor's SYRK updated (N = 1024, 2048: nodes read from S); N = 500 pads the last
+    tile.  So the form is a launch choice only (GPRX_OPT_NODE_WAVES)."""
+    from gprx import _lib as L, data
+
+    G = 26 if mech == "CP" else 6
+    trs = [data.make_trial(mech, N, 40, seed=data.trial_seed(mech, 60 + t)) for t in range(B // G + 1)]
+    X = np.stack([trs[s // G]["X"] for s in range(B)])
+    Y = np.stack([(trs[s // G]["Xcurr"] if mech == "CP" else trs[s // G]["Y"])[s % G] for s in range(B)])
+    Xs = np.stack([trs[s // G]["Xs"] for s in range(B)])
+    X[3][:, 100] = np.nan
+    X[B - 2][:, 300] = np.nan
+    rng = np.random.default_rng(N + B)
+    th0 = data.theta0(mech, 512)
+    T = np.stack([th0 + 0.05 * rng.standard_normal(th0.shape[0]) for _ in range(B)])
+    b = gprx.GPBatch(B, 26, N, 40, ctx=ctx)
+    b.set_train(X, Y)
+    b.set_test(Xs)
+    out = {}
+    try:
+        for w in (8, 4):
+            ctx.set_option(L.OPT_NODE_WAVES, w)
+            out[w] = b.run(T, grad=True, predict=True)
+    finally:
+        ctx.set_option(L.OPT_NODE_WAVES, 0)
+    assert out[4]["status"][3] == 1 and out[4]["info"][3] == 101
+    assert out[4]["status"][B - 2] == 1 and out[4]["info"][B - 2] == 301
+    assert np.sum(out[4]["status"] == 0) == B - 2
+    for k in ("mll", "grad", "mu", "var", "status", "info"):
+        np.testing.assert_array_equal(out[4][k], out[8][k], err_msg=k)
+    ok = np.nonzero(out[4]["status"] == 0)[0]
+    check_slot(out[4], int(ok[0]), X[ok[0]], Y[ok[0]], T[ok[0]], Xs[ok[0]], ctx.dist_mode, strict=mech != "CP")
+    b.close()
+
+
 def test_production_path_b32_full_size(gprx, ctx):
     """The bench's configuration: B >= 32 slots (fused 256x256 leaves, folded 64x64 GEMM units,
     folded lauum jobs) at N=2048, d=26, M=100; three slots against the oracle, all slots finite
