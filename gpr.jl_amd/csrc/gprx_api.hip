@@ -243,7 +243,6 @@ int copy_in(gprx_ctx* c, void* dst, const void* src, size_t bytes, int mem) {
 // Recursive Cholesky + inverse over tile range [o, o+n) (tile units), all slots in lock step.
 // upd: the node lies in the trailing block of an ancestor (its tiles were updated into S); the top
 // child inherits the parent's flag, the bottom child follows the parent's SYRK
-constexpr int NODE8H_MIN_SLOTS = 512;  // auto: k_node8h from two slots per CU on 256 CUs
 void factor_rec(gprx_ctx* c, hipStream_t st, const DevBatch& db, int o, int n, int upd) {
   const double T = TS, Bd = db.B;
   const int leaf = c->leaf_tiles > 0 ? c->leaf_tiles : (db.B >= 32 ? 4 : 1);
@@ -258,8 +257,10 @@ void factor_rec(gprx_ctx* c, hipStream_t st, const DevBatch& db, int o, int n, i
 #endif
   if (GPRX_NODE8 && n == 8 && leaf == 4 && db.B >= 32) {  // the whole node in one launch (k_node8)
     const double m = 4 * T;
-    // the 4-wave form (two slots per CU) when the slots outnumber the CUs by far; bit-identical
-    const bool four = c->node_waves == 4 || (c->node_waves == 0 && db.B >= NODE8H_MIN_SLOTS);
+    // the 4-wave form (two slots per CU, bit-identical) on request only: measured slower at every
+    // batch size ("Two slots per CU"): a paired slot's fp64 VALU chain and MFMAs share
+    // the SIMD's one fp64 pipe with the other slot's, so the pair runs at half speed
+    const bool four = c->node_waves == 4;
     timed(c, st, four ? "node8h" : "node8", Bd * (4.0 * m * m * m / 3.0 + 4.0 * m * m * m),
           Bd * 8.0 * (16.0 * m * m + 6.5 * m * m), [&] { gprx::launch_node8(db, o, upd, st, four); }, n);
     return;

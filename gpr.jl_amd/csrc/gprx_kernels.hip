@@ -858,7 +858,21 @@ __device__ __forceinline__ void wave_ts(int o, int slot, int ev) {
   }
 }
 #define W_TS(ev) wave_ts(o, slot, ev)
+// whole-node kernels (k_node8 / k_node8h): thread 0 stamps phase ev of slot's node launch (region
+// 0 from entry 2^19: 8 per slot: start, after the top leaf, TRSM, SYRK + TT, the bottom leaf, end,
+// then the hardware CU id and XCC id)
+__device__ __forceinline__ void node_ts(int slot, int ev) {
+  if (threadIdx.x == 0 && slot < 32768) {
+    unsigned long long t = __builtin_amdgcn_s_memrealtime();
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    if (ev == 6) t = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));
+    if (ev == 7) t = __builtin_amdgcn_s_getreg((20) | (0 << 6) | (15 << 11));
+    (&g_stamps[0][0][0])[524288 + (size_t)slot * 8 + ev] = t;
+  }
+}
+#define N_TS(ev) node_ts(slot, ev)
 #else
+#define N_TS(ev)
 #define D_TS1(ev)
 #define LEAF_TS(ev)
 #define L9_TS(ev)
@@ -2668,15 +2682,23 @@ __global__ __launch_bounds__(2 * NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))
   if (slot >= db.B || !slot_active(db, slot)) return;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), half = wave >> 2, w = wave & 3;
   const GemmGeom none{OP_NONE, 0, 0, 0};
+  N_TS(0);
+  N_TS(6);
+  N_TS(7);
   leaf9_body(db, o, upd);
   __syncthreads();
+  N_TS(1);
   gemm_unit<false, REV_B, false>(db, GemmGeom{OP_TRSM, o, 4, 8, upd}, none, slot, half, w, 2);
   __syncthreads();
+  N_TS(2);
   gemm_unit<false, TRI_A_FIRST, false>(db, GemmGeom{OP_SYRK, o, 4, 8, upd}, GemmGeom{OP_TT, o, 4, 8, upd}, slot, half, w, 2);
   __syncthreads();
+  N_TS(3);
   leaf9_body(db, o + 4, 1);
   __syncthreads();
+  N_TS(4);
   gemm_unit<false, REV_A, false>(db, GemmGeom{OP_LINV21, o, 4, 8, upd}, none, slot, half, w, 2);
+  N_TS(5);
 }
 
 // ============================================================================================
@@ -2686,7 +2708,11 @@ __global__ __launch_bounds__(2 * NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))
 // chain products, the task items' operand round trips) that leave the CU's MFMA pipes mostly idle,
 // and a launch of more slots than CUs (the CP batches, the sweeps' and searches' N = 512 .. 2048
 // groups) runs them round after round.  With two slots per CU one slot's leaf latency overlaps the
-// other's GEMM phases.  Every product, sum and store is k_node8's, in the same order: the results
+// other's GEMM phases -- the plan; measured (scratch/node_timeline.py), a paired slot runs every
+// phase, its leaves included, at about half its solo speed: the diagonal wave's fp64 VALU chain and
+// the items' MFMAs share each SIMD's one fp64 pipe with the other slot's MFMAs, so the pair gains
+// nothing ("Two slots per CU").  Kept as an option (GPRX_OPT_NODE_WAVES = 4), off by
+// default.  Every product, sum and store is k_node8's, in the same order: the results
 // are bit-identical (tests/test_gpu.py::test_node8_four_wave_form_bit_identical), so the launch
 // form never changes a result and the batch-size rule of set_geometry stays the only geometry one.
 // What changes against leaf9_body:
@@ -3099,19 +3125,27 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
 #endif
   // workgroups b and b + 256 tend to share a CU (256 CUs filled in block order)
   const int rot = GPRX_N8H_ROT == 1 ? ((blockIdx.x >> 8) & 1) * 2 : 0;
+  N_TS(0);
+  N_TS(6);
+  N_TS(7);
   leaf4_body(db, o, upd, rot);
   __syncthreads();
+  N_TS(1);
 #pragma unroll 1
   for (int u = 0; u < 2; ++u) gemm_unit<false, REV_B, false>(db, GemmGeom{OP_TRSM, o, 4, 8, upd}, none, slot, u, wave, 2);
   __syncthreads();
+  N_TS(2);
 #pragma unroll 1
   for (int u = 0; u < 2; ++u)
     gemm_unit<false, TRI_A_FIRST, false>(db, GemmGeom{OP_SYRK, o, 4, 8, upd}, GemmGeom{OP_TT, o, 4, 8, upd}, slot, u, wave, 2);
   __syncthreads();
+  N_TS(3);
   leaf4_body(db, o + 4, 1, rot);
   __syncthreads();
+  N_TS(4);
 #pragma unroll 1
   for (int u = 0; u < 2; ++u) gemm_unit<false, REV_A, false>(db, GemmGeom{OP_LINV21, o, 4, 8, upd}, none, slot, u, wave, 2);
+  N_TS(5);
 }
 
 

@@ -102,8 +102,8 @@ int gprx_ctx_set_profiling(gprx_ctx* ctx, int enable);
  *   GPRX_OPT_SMALL_N     recursion nodes of <= value tiles use the 64 x 32 pair-unit GEMM; 0 = auto
  *   GPRX_OPT_GRAPHS      1: replay each evaluation's launch sequence as a hipGraph (default 0)
  *   GPRX_OPT_NODE_WAVES  the whole-8-tile-node kernel (batches >= 32 slots): 8 = one 8-wave
- *                        workgroup per slot, 4 = a 4-wave workgroup per slot (two slots per CU);
- *                        0 (default) = auto (4 from 512 slots)                                   */
+ *                        workgroup per slot (0, the default, is 8); 4 = a 4-wave workgroup per
+ *                        slot, two slots per CU (measured slower on MI355X)          */
 #define GPRX_OPT_LEAF_TILES 1
 #define GPRX_OPT_SMALL_N 2
 #define GPRX_OPT_GRAPHS 3
