@@ -2244,8 +2244,19 @@ struct Leaf9Sync {
   int crit;        // critical SYRK items done (monotonic over the steps)
 };
 constexpr int L9_TW = 7;
-// position of task wave w in l9_wave_of's round robin (5, 6, 7, 1, 2, 3, 4)
-__device__ __forceinline__ int l9_pos(int w) { return w >= 5 ? w - 5 : (w <= 3 ? w + 2 : 6); }
+// Items go round the task waves (L9_HW of them), the three off the chain first: 5, 6, 7, 1, 2, 3
+// (round 6: L9_HW = 6), or 5, 6, 7, 1, 2, 3, 4 (L9_HW = 7, rounds 4-5).  Wave 4 is the diagonal
+// wave's SIMD-mate (waves w and w + 4 of a workgroup share a SIMD, scratch/hwid_probe.hip), and the
+// fp64 VALU of the diagonal routine shares that SIMD's one fp64 pipe with the mate's MFMAs: without
+// items on wave 4 (it keeps its chain quarter, while wave 0 waits), node8 2.741 -> 2.723 ms per
+// step at B = 240 and 2.998 -> 2.957 ms for CP at B = 1014 (same box, two pairs each; the same
+// items, so bit-identical).
+#ifndef GPRX_L9_HW
+#define GPRX_L9_HW 6
+#endif
+constexpr int L9_HW = GPRX_L9_HW;
+// position of task wave w in l9_wave_of's round robin (-1: no items)
+__device__ __forceinline__ int l9_pos(int w) { return w >= 5 ? w - 5 : (w <= 3 ? w + 2 : (L9_HW == 7 ? 6 : -1)); }
 // phase B of step k (m = n - 1 - k trailing tiles per edge): the SYRK tiles the next step needs,
 // column k + 1 below the diagonal and the next diagonal tile, are its first nc tiles in the
 // column-major enumeration that skips (k + 1, k + 1)
@@ -2264,9 +2275,8 @@ __device__ __forceinline__ void lds_count(int* p) {  // one more item done (its 
   l9_release();
   if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(p, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-// Items go round the task waves, the three off the chain first (waves 5, 6, 7, then 1, 2, 3, 4);
-// the diagonal tile's four store quarters go to waves 4..7.
-constexpr int L9_HW = 7;
+// The diagonal tile's four store quarters go to waves 4..7 (L9_HW = 6: 1, 5, 6, 7).
+__device__ __forceinline__ int l9_store_wave(int e) { return L9_HW == 7 || e > 0 ? 4 + e : 1; }
 __device__ __forceinline__ int l9_wave_of(int e) {
   const int r = e % L9_HW;
   return r < 3 ? 5 + r : (r < 6 ? r - 2 : 4);
@@ -2440,7 +2450,7 @@ __device__ __forceinline__ void leaf9_body(const DevBatch& db, int o, int upd) {
       // items of Y(k, j) held since the previous step: e = 4 j + c, phase-B item g = nc4p + e on
       // wave l9_wave_of(g); this wave's h-th one is g = g0 + 7 h (g0: its first g >= nc4p)
       const int nyp = 4 * k;  // Y(k, j), j < k
-      const int g0p = nc4p + ((rw - nc4p) % 7 + 7) % 7;
+      const int g0p = nc4p + ((rw - nc4p) % L9_HW + L9_HW) % L9_HW;
       lds_wait_gt(&sy.diag_done, k, db, slot);
       if (wave == 5) L9_TS(9 + 4 * k);
       // ---- phase A: the chain; the held inverse items of row k; the diagonal tile's stores; the
@@ -2492,8 +2502,8 @@ __device__ __forceinline__ void leaf9_body(const DevBatch& db, int o, int upd) {
       // held items: X(k, j) = -Linv_kk Y(k, j), columns cq.. of tile (kk, o + j)
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const int e = g0p + 7 * h - nc4p;
-        if (e < nyp) {
+        const int e = g0p + L9_HW * h - nc4p;
+        if (rw >= 0 && e < nyp) {
           const int j = e >> 2, c = e & 3, tj = o + j, xq = 16 * c;
           double b[16];
 #pragma unroll
@@ -2527,7 +2537,7 @@ __device__ __forceinline__ void leaf9_body(const DevBatch& db, int o, int upd) {
         const int na = 4 + 4 * nt1;
         bool waited = false;
         for (int e = 0; e < na; ++e) {
-          if ((e < 4 ? 4 + e : l9_wave_of(nyp + e - 4)) != wave) continue;
+          if ((e < 4 ? l9_store_wave(e) : l9_wave_of(nyp + e - 4)) != wave) continue;
           const int c = e & 3, xq = 16 * c;
           if (e >= 4 && !waited) {  // S(ti, kk): the previous step's critical items
             lds_wait_ge(&sy.crit, ncrit, db, slot);
@@ -2609,15 +2619,15 @@ __device__ __forceinline__ void leaf9_body(const DevBatch& db, int o, int upd) {
             for (int q = 0; q < 4; ++q) S[(tj * TS + 16 * a + 4 * q) * ldi + ti * TS + xq + lo] = -acc[a][q];
           W_TS(8 * k + 1 + (nb < 5 ? nb++ : 5));
         };
-        for (int g = (rw - 0 + 7) % 7; g < nc4; g += 7) {
+        for (int g = rw < 0 ? nc4 : rw; g < nc4; g += L9_HW) {
           syrk_item(g);
           lds_count(&sy.crit);
         }
-        const int g0 = nc4 + ((rw - nc4) % 7 + 7) % 7;
+        const int g0 = nc4 + ((rw - nc4) % L9_HW + L9_HW) % L9_HW;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          const int e = g0 + 7 * h - nc4;
-          if (e < ny) {
+          const int e = g0 + L9_HW * h - nc4;
+          if (rw >= 0 && e < ny) {
             const int j = e >> 2, c = e & 3, tj = o + j, xq = 16 * c;
             // Y(k1, tj)[:, xq..] = sum_{m=tj}^{kk} L(k1, m) Linv(m, tj): M = Lw row k1, N = Mt row tj
             // (Linv(m, tj)^T); Linv(tj, tj)'s columns xq.. are zero above row xq: K starts at xq
@@ -2627,7 +2637,8 @@ __device__ __forceinline__ void leaf9_body(const DevBatch& db, int o, int upd) {
             W_TS(8 * k + 1 + (nb < 5 ? nb++ : 5));
           }
         }
-        for (int g = nc4 + ny + ((rw - nc4 - ny) % 7 + 7) % 7; g < 4 * nsy + ny; g += 7) syrk_item(g - ny);
+        for (int g = rw < 0 ? 4 * nsy + ny : nc4 + ny + ((rw - nc4 - ny) % L9_HW + L9_HW) % L9_HW; g < 4 * nsy + ny; g += L9_HW)
+          syrk_item(g - ny);
         W_TS(8 * k + 7);
         ncrit += nc4;
         nc4p = nc4;
