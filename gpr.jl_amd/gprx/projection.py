@@ -125,14 +125,26 @@ def predictdynamics(mech: str, groups, start, steps: int, vw_indices, regularize
 
 
 def _default_ctx():
-    """The context of this rank's device: GPU LOCAL_RANK (mod the visible devices, as
-    shard.init_ranks binds a rank; 0 without a launcher).  Read from the environment, not from
-    torch, so that a library call without a ctx neither initialises torch's HIP runtime nor picks a
-    device other than the one the rank's own contexts use."""
+    """The context of this process's device, in this order:
+      * GPRX_DEVICE (an explicit device index);
+      * torch's current device, when this process has already initialised torch's HIP runtime (a
+        caller that chose a GPU with torch.cuda.set_device(k) keeps it; nothing is initialised here);
+      * GPU LOCAL_RANK (mod the visible devices, as shard.init_ranks binds a rank; 0 without a
+        launcher)."""
     import os
+    import sys
 
     from .batch import default_context
 
-    n = int(L.lib.gprx_device_count())
-    dev = int(os.environ.get("LOCAL_RANK", "0") or 0) % max(1, n)
-    return default_context(dev)
+    return default_context(default_device(int(L.lib.gprx_device_count()), os.environ, sys.modules.get("torch")))
+
+
+def default_device(ndev: int, env, torch=None) -> int:
+    """_default_ctx's device index (ndev visible devices, env a mapping, torch the imported module
+    or None)."""
+    n = max(1, int(ndev))
+    if str(env.get("GPRX_DEVICE", "")).strip():
+        return int(env["GPRX_DEVICE"]) % n
+    if torch is not None and torch.cuda.is_initialized():
+        return int(torch.cuda.current_device()) % n
+    return int(env.get("LOCAL_RANK", "0") or 0) % n

@@ -198,3 +198,32 @@ def test_device_max_rollout_matches_oracle(mech):
     assert np.all(np.abs(out - ref) <= tol), float(np.max(np.abs(out - ref) / tol))
     np.testing.assert_allclose(pe, pref, rtol=1e-6, atol=1e-12)
     b.close()
+
+
+def test_default_device_choice():
+    """projection._default_ctx's device: GPRX_DEVICE, else torch's current device when
+    torch's HIP runtime is already initialised (torch.cuda.set_device is honoured), else LOCAL_RANK
+    modulo the visible devices; no runtime is initialised by the lookup."""
+    from gprx.projection import default_device
+
+    class FakeCuda:
+        def __init__(self, init, cur):
+            self.init, self.cur = init, cur
+
+        def is_initialized(self):
+            return self.init
+
+        def current_device(self):
+            return self.cur
+
+    class FakeTorch:
+        def __init__(self, init, cur):
+            self.cuda = FakeCuda(init, cur)
+
+    assert default_device(8, {}) == 0
+    assert default_device(8, {"LOCAL_RANK": "5"}) == 5
+    assert default_device(4, {"LOCAL_RANK": "5"}) == 1
+    assert default_device(8, {"LOCAL_RANK": "5"}, FakeTorch(False, 3)) == 5
+    assert default_device(8, {"LOCAL_RANK": "5"}, FakeTorch(True, 3)) == 3
+    assert default_device(8, {"LOCAL_RANK": "5", "GPRX_DEVICE": "6"}, FakeTorch(True, 3)) == 6
+    assert default_device(0, {"GPRX_DEVICE": "2"}) == 0
