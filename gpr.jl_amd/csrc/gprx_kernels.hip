@@ -885,6 +885,15 @@ __device__ __forceinline__ void node_ts(int slot, int ev) {
 constexpr int GTS_MAX = 1 << 17;
 __device__ unsigned long long g_gts[GTS_MAX][8];
 __device__ __forceinline__ void gts(const GemmGeom& g, int pass, int ev) {
+  if (GPRX_GSTAMPS == 1208) {  // k_node8's SYRK + TT phase: every wave (8 per block), 4 tiles, 4 events
+    if (!((g.op == OP_SYRK || g.op == OP_TT) && g.n == 8) || pass > 3 || blockDim.x != 512) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    const size_t i = (size_t)blockIdx.x * 8 + (threadIdx.x >> 6);
+    if ((threadIdx.x & 63) == 0 && 2 * i + 1 < GTS_MAX) (&g_gts[0][0])[i * 16 + 4 * pass + ev] = t;
+    return;
+  }
   if (g.op * 100 + g.n != GPRX_GSTAMPS || pass > 1) return;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const unsigned long long t = __builtin_amdgcn_s_memrealtime();
@@ -1521,10 +1530,15 @@ __device__ __forceinline__ void gemm_tile(const DevBatch& db, const GemmGeom& g,
 // The SYRK + TT launch of an 8-tile node (m1 = m2 = 4 tiles): 10 SYRK tiles of K = 4 tiles and 16 TT
 // tiles of K = 4 - i (row i), 80 tile-K in all.  The unit decomposition below gives 5 workgroups
 // per slot (1200 at B = 240: 2.34 rounds of 512 resident workgroups, i.e. three); this fixed plan
-// packs them into 2 workgroups per slot, every wave a list of 3-4 tiles summing to 10 tile-K (one
-// round).  Entry: sel * 16 + 4 i + j, tile (i, j) of the SYRK (sel 0) or TT (sel 1) rectangle.
-__constant__ int N8_PLAN[8][4] = {{0, 4, 24, -1},  {5, 8, 25, -1},  {9, 10, 26, -1},  {12, 13, 27, -1},
-                                   {14, 20, 21, -1}, {15, 22, 23, -1}, {16, 17, 28, 29}, {18, 19, 30, 31}};
+// packs them into 2 workgroups per slot (one round), every wave a list of 3-4 tiles.  Round 6: the
+// lists balance issued MFMAs, not tile-K (a diagonal SYRK tile forms 10 of its 16 blocks, a TT
+// tile skips 96 of its first K tile's 256 MFMAs): 2112-2240 MFMAs per wave, and 4352 on each SIMD,
+// whose two waves are w and w + 4 in k_node8 (scratch/hwid_probe.hip); the round-5 lists had
+// 1984-2464 per wave and 4064-4640 per SIMD, and k_node8's SYRK + TT phase ended 45 us apart on a
+// slot's waves (scratch/node8_gts.py).  Entry: sel * 16 + 4 i + j, tile (i, j) of the SYRK (sel 0)
+// or TT (sel 1) rectangle, each list longest first.
+__constant__ int N8_PLAN[8][4] = {{13, 18, 30, -1}, {17, 20, 0, -1},  {8, 10, 24, 28}, {19, 22, 15, -1},
+                                   {9, 5, 27, 31},   {14, 21, 26, -1}, {12, 23, 25, -1}, {4, 16, 29, -1}};
 __host__ __device__ inline bool n8_plan(const GemmGeom& g1, const GemmGeom& g2) {
   return g1.op == OP_SYRK && g2.op == OP_TT && g1.n == 8 && g1.h == 4;
 }
