@@ -15,8 +15,8 @@ import gprx  # noqa: E402
 from gprx import data  # noqa: E402
 
 ctx = gprx.Context(0)
-cases = [("P1", 50, 64, 3, 256), ("CP", 512, 512, 26, 8), ("CP", 512, 512, 26, 16), ("CP", 512, 512, 26, 24),
-         ("CP", 512, 512, 26, 32), ("P2", 2048, 2048, 6, 40), ("FB", 4096, 512, 12, 4), ("FB", 4096, 512, 12, 8)]
+cases = [("P1", 50, 64, 3, 256), ("CP", 512, 512, 26, 8), ("CP", 512, 512, 26, 19), ("CP", 512, 512, 26, 39),
+         ("CP", 512, 512, 26, 59), ("P2", 2048, 2048, 6, 40), ("FB", 4096, 512, 12, 4), ("FB", 4096, 512, 12, 8)]
 if "--cp" in sys.argv:
     i = sys.argv.index("--cp")
     cases = [("CP", 512, 512, 26, int(t)) for t in sys.argv[i + 1].split(",")]
