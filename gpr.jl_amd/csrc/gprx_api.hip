@@ -687,6 +687,26 @@ int gprx_batch_set_test(gprx_batch* b, const double* Xs, int M, int64_t xss, int
   return GPRX_OK;
 }
 
+// Page-locked host memory (hipHostMalloc / registered, e.g. torch's pinned tensors): the device
+// writes it by DMA, so the predictive outputs can go straight into the caller's buffer (one
+// pitched copy) instead of through the batch's staging buffer and a host copy per slot.
+static bool pinned_host(const void* p) {
+  if (!p) return false;
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();  // pageable memory: not known to the runtime
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+// queue the copy of a [B][Mpad] device output to the caller's [B][M] buffer when it is pinned;
+// returns whether it did (else the caller stages it)
+static bool out_direct(gprx_ctx* c, double* dst, const double* src, const DevBatch& db) {
+  if (!pinned_host(dst)) return false;
+  return hipMemcpy2DAsync(dst, (size_t)db.M * sizeof(double), src, (size_t)db.Mpad * sizeof(double), (size_t)db.M * sizeof(double),
+                          db.B, hipMemcpyDeviceToHost, c->stream) == hipSuccess;
+}
+
 static int batch_predict_locked(gprx_batch* b, double* mu, double* var) {
   gprx_ctx* c = b->ctx;
   DevBatch& db = b->db;
@@ -695,13 +715,16 @@ static int batch_predict_locked(gprx_batch* b, double* mu, double* var) {
   db.want_var = var != nullptr;
   int rc = run_eval(b, false, true, false);
   if (rc) return rc;
-  HIPCHK(c, hipMemcpyAsync(b->h_mu, db.out_mu, (size_t)db.B * db.Mpad * sizeof(double), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipMemcpyAsync(b->h_var, db.out_var, (size_t)db.B * db.Mpad * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  const bool dmu = mu && out_direct(c, mu, db.out_mu, db), dvar = var && out_direct(c, var, db.out_var, db);
+  if (mu && !dmu)
+    HIPCHK(c, hipMemcpyAsync(b->h_mu, db.out_mu, (size_t)db.B * db.Mpad * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  if (var && !dvar)
+    HIPCHK(c, hipMemcpyAsync(b->h_var, db.out_var, (size_t)db.B * db.Mpad * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   collect(c);
   for (int s = 0; s < db.B; ++s) {
-    if (mu) memcpy(mu + (size_t)s * db.M, b->h_mu + (size_t)s * db.Mpad, db.M * sizeof(double));
-    if (var) memcpy(var + (size_t)s * db.M, b->h_var + (size_t)s * db.Mpad, db.M * sizeof(double));
+    if (mu && !dmu) memcpy(mu + (size_t)s * db.M, b->h_mu + (size_t)s * db.Mpad, db.M * sizeof(double));
+    if (var && !dvar) memcpy(var + (size_t)s * db.M, b->h_var + (size_t)s * db.Mpad, db.M * sizeof(double));
   }
   return GPRX_OK;
 }
@@ -733,9 +756,14 @@ int gprx_batch_run(gprx_batch* b, const double* theta, unsigned flags, double* m
   }
   HIPCHK(c, hipMemcpyAsync(b->h_out, db.out, (size_t)B * (d + 3) * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipMemcpyAsync(b->h_status, db.status, 2 * (size_t)B * sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  bool dmu = false, dvar = false;  // predictive outputs copied straight into pinned caller buffers
   if (want_pred) {
-    HIPCHK(c, hipMemcpyAsync(b->h_mu, db.out_mu, (size_t)B * db.Mpad * sizeof(double), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(b->h_var, db.out_var, (size_t)B * db.Mpad * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    dmu = mu && out_direct(c, mu, db.out_mu, db);
+    dvar = var && out_direct(c, var, db.out_var, db);
+    if (mu && !dmu)
+      HIPCHK(c, hipMemcpyAsync(b->h_mu, db.out_mu, (size_t)B * db.Mpad * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    if (var && !dvar)
+      HIPCHK(c, hipMemcpyAsync(b->h_var, db.out_var, (size_t)B * db.Mpad * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));
   collect(c);
@@ -749,8 +777,8 @@ int gprx_batch_run(gprx_batch* b, const double* theta, unsigned flags, double* m
     if (mll) mll[s] = o[0];
     if (grad && want_grad) memcpy(grad + (size_t)s * np, o + 1, np * sizeof(double));
     if (want_pred) {
-      if (mu) memcpy(mu + (size_t)s * db.M, b->h_mu + (size_t)s * db.Mpad, db.M * sizeof(double));
-      if (var) memcpy(var + (size_t)s * db.M, b->h_var + (size_t)s * db.Mpad, db.M * sizeof(double));
+      if (mu && !dmu) memcpy(mu + (size_t)s * db.M, b->h_mu + (size_t)s * db.Mpad, db.M * sizeof(double));
+      if (var && !dvar) memcpy(var + (size_t)s * db.M, b->h_var + (size_t)s * db.Mpad, db.M * sizeof(double));
     }
   }
   b->factored = true;

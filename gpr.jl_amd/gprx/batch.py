@@ -90,6 +90,20 @@ def _f64(a):
     return np.ascontiguousarray(a, dtype=np.float64)
 
 
+def host_empty(shape) -> np.ndarray:
+    """An fp64 host array for per-test-point outputs, page-locked when torch's HIP runtime is
+    usable (its caching pinned allocator: no allocation cost after the first calls), so that the
+    library copies the predictive mean / variance straight into it by DMA; else plain numpy."""
+    try:
+        import torch
+
+        if torch.cuda.is_available():
+            return torch.empty(shape, dtype=torch.float64, pin_memory=True).numpy()
+    except Exception:  # noqa: BLE001 -- any failure: pageable memory, the library stages the copy
+        pass
+    return np.empty(shape)
+
+
 def opt_options(method=None, options=None, refit: bool = True) -> "L.OptOptions":
     """gprx_opt_options from gprx.optim.LBFGS / Options, validated here (ValueError) with the same
     bounds gprx_batch_optimize enforces, so a rejected call never reaches the library."""
@@ -193,8 +207,8 @@ class GPBatch:
         mll = np.empty(self.B)
         g = np.empty((self.B, self.d + 2)) if grad else None
         pred = predict and self.M > 0
-        mu = np.empty((self.B, self.M)) if pred else None
-        var = np.empty((self.B, self.M)) if pred and variance else None
+        mu = host_empty((self.B, self.M)) if pred else None
+        var = host_empty((self.B, self.M)) if pred and variance else None
         st = np.empty(self.B, dtype=np.int32)
         info = np.empty(self.B, dtype=np.int32)
         flags = (L.WANT_GRAD if grad else 0) | (L.WANT_PREDICT if pred else 0)
@@ -253,8 +267,8 @@ class GPBatch:
     def predict(self, variance: bool = True):
         """Predictive mean (and variance) at the current test points from the last run's
         factorisation; variance=False returns (mu, None) without the variance GEMM."""
-        mu = np.empty((self.B, self.M))
-        var = np.empty((self.B, self.M)) if variance else None
+        mu = host_empty((self.B, self.M))
+        var = host_empty((self.B, self.M)) if variance else None
         L.check(L.lib.gprx_batch_predict(self.h, L.dptr(mu), L.dptr(var)), self.ctx.h)
         return mu, var
 
