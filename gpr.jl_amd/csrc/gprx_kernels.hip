@@ -2269,8 +2269,15 @@ constexpr int L9_TW = 7;
 #define GPRX_L9_HW 6
 #endif
 constexpr int L9_HW = GPRX_L9_HW;
-// position of task wave w in l9_wave_of's round robin (-1: no items)
-__device__ __forceinline__ int l9_pos(int w) { return w >= 5 ? w - 5 : (w <= 3 ? w + 2 : (L9_HW == 7 ? 6 : -1)); }
+// Phase B (the SYRK items and the Y items of the next inverse row) runs while the diagonal wave
+// waits for the next chain, so its round robin keeps wave 4 (L9_HWB = 7): otherwise its SIMD idles
+// through phase B.
+#ifndef GPRX_L9_HWB
+#define GPRX_L9_HWB 7
+#endif
+constexpr int L9_HWB = GPRX_L9_HWB;
+// position of task wave w in a round robin over nw task waves (-1: no items)
+__device__ __forceinline__ int l9_pos(int w, int nw = L9_HW) { return w >= 5 ? w - 5 : (w <= 3 ? w + 2 : (nw == 7 ? 6 : -1)); }
 // phase B of step k (m = n - 1 - k trailing tiles per edge): the SYRK tiles the next step needs,
 // column k + 1 below the diagonal and the next diagonal tile, are its first nc tiles in the
 // column-major enumeration that skips (k + 1, k + 1)
@@ -2454,7 +2461,7 @@ __device__ __forceinline__ void leaf9_body(const DevBatch& db, int o, int upd) {
       for (int s = 0; s < 16; ++s) Bs[4 * s * FS + cq + llo] = v[s];
     };
     if (cw >= 0) preload(0);
-    const int rw = l9_pos(wave);
+    const int rw = l9_pos(wave, L9_HWB);  // phase B (and the held inverse items)
     int ncrit = 0;  // critical SYRK items of the steps so far (sy.crit's target)
     int nc4p = 0;   // critical items of the previous step's phase B (the held items' offset)
     for (int k = 0; k < n; ++k) {
@@ -2464,7 +2471,7 @@ __device__ __forceinline__ void leaf9_body(const DevBatch& db, int o, int upd) {
       // items of Y(k, j) held since the previous step: e = 4 j + c, phase-B item g = nc4p + e on
       // wave l9_wave_of(g); this wave's h-th one is g = g0 + 7 h (g0: its first g >= nc4p)
       const int nyp = 4 * k;  // Y(k, j), j < k
-      const int g0p = nc4p + ((rw - nc4p) % L9_HW + L9_HW) % L9_HW;
+      const int g0p = nc4p + ((rw - nc4p) % L9_HWB + L9_HWB) % L9_HWB;
       lds_wait_gt(&sy.diag_done, k, db, slot);
       if (wave == 5) L9_TS(9 + 4 * k);
       // ---- phase A: the chain; the held inverse items of row k; the diagonal tile's stores; the
@@ -2516,7 +2523,7 @@ __device__ __forceinline__ void leaf9_body(const DevBatch& db, int o, int upd) {
       // held items: X(k, j) = -Linv_kk Y(k, j), columns cq.. of tile (kk, o + j)
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const int e = g0p + L9_HW * h - nc4p;
+        const int e = g0p + L9_HWB * h - nc4p;
         if (rw >= 0 && e < nyp) {
           const int j = e >> 2, c = e & 3, tj = o + j, xq = 16 * c;
           double b[16];
@@ -2633,14 +2640,14 @@ __device__ __forceinline__ void leaf9_body(const DevBatch& db, int o, int upd) {
             for (int q = 0; q < 4; ++q) S[(tj * TS + 16 * a + 4 * q) * ldi + ti * TS + xq + lo] = -acc[a][q];
           W_TS(8 * k + 1 + (nb < 5 ? nb++ : 5));
         };
-        for (int g = rw < 0 ? nc4 : rw; g < nc4; g += L9_HW) {
+        for (int g = rw < 0 ? nc4 : rw; g < nc4; g += L9_HWB) {
           syrk_item(g);
           lds_count(&sy.crit);
         }
-        const int g0 = nc4 + ((rw - nc4) % L9_HW + L9_HW) % L9_HW;
+        const int g0 = nc4 + ((rw - nc4) % L9_HWB + L9_HWB) % L9_HWB;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          const int e = g0 + L9_HW * h - nc4;
+          const int e = g0 + L9_HWB * h - nc4;
           if (rw >= 0 && e < ny) {
             const int j = e >> 2, c = e & 3, tj = o + j, xq = 16 * c;
             // Y(k1, tj)[:, xq..] = sum_{m=tj}^{kk} L(k1, m) Linv(m, tj): M = Lw row k1, N = Mt row tj
@@ -2651,7 +2658,7 @@ __device__ __forceinline__ void leaf9_body(const DevBatch& db, int o, int upd) {
             W_TS(8 * k + 1 + (nb < 5 ? nb++ : 5));
           }
         }
-        for (int g = rw < 0 ? 4 * nsy + ny : nc4 + ny + ((rw - nc4 - ny) % L9_HW + L9_HW) % L9_HW; g < 4 * nsy + ny; g += L9_HW)
+        for (int g = rw < 0 ? 4 * nsy + ny : nc4 + ny + ((rw - nc4 - ny) % L9_HWB + L9_HWB) % L9_HWB; g < 4 * nsy + ny; g += L9_HWB)
           syrk_item(g - ny);
         W_TS(8 * k + 7);
         ncrit += nc4;
