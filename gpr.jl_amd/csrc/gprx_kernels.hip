@@ -2461,7 +2461,14 @@ __device__ __forceinline__ void leaf9_body(const DevBatch& db, int o, int upd) {
       for (int s = 0; s < 16; ++s) Bs[4 * s * FS + cq + llo] = v[s];
     };
     if (cw >= 0) preload(0);
-    const int rw = l9_pos(wave, L9_HWB);  // phase B (and the held inverse items)
+#ifndef GPRX_L9_BORDER
+#define GPRX_L9_BORDER 1
+#endif
+    // phase B (and the held inverse items): round-robin position.  BORDER 1: waves 4, 1, 2, 3 first
+    // (wave 4 alone on its SIMD while wave 0 waits; waves 5-7 share SIMDs with the older waves 1-3,
+    // which win issue arbitration: a younger wave's first item took 18-20 us against 10-11 us in the
+    // leaf timeline), so the critical items land on the waves that run them fastest
+    const int rw = GPRX_L9_BORDER ? (wave == 4 ? 0 : (wave <= 3 ? wave : wave - 1)) : l9_pos(wave, L9_HWB);
     int ncrit = 0;  // critical SYRK items of the steps so far (sy.crit's target)
     int nc4p = 0;   // critical items of the previous step's phase B (the held items' offset)
     for (int k = 0; k < n; ++k) {
