@@ -2,16 +2,16 @@
 # leaf phase B over 7 task waves (in-tree) against 6 (hwb6)
 set -e
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu.py -k "n8_plan or four_wave or fused_node or production or factorisation_paths or small or full_size" > gpurun_out/r6_bord_tests.txt 2>&1
-tail -n 1 gpurun_out/r6_bord_tests.txt
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu.py -k "n8_plan or four_wave or fused_node or production or factorisation_paths or small or full_size" > gpurun_out/r6_defer_tests.txt 2>&1
+tail -n 1 gpurun_out/r6_defer_tests.txt
 for i in 1 2; do
-  for v in in-tree bord0; do
+  for v in in-tree defer0; do
     if [ $v = in-tree ]; then unset GPRX_LIB; else export GPRX_LIB=scratch/var/libgprx_$v.so; fi
-    timeout -k 10 300 python scratch/levels.py 40 3 > gpurun_out/r6_bord_${v}_p2$i.txt 2>&1
-    timeout -k 10 300 python scratch/levels_cfg.py CP 512 512 26 39 5 > gpurun_out/r6_bord_${v}_cp$i.txt 2>&1
-    echo "$v $i p2 node8 $(grep node8 gpurun_out/r6_bord_${v}_p2$i.txt | awk '{print $2}') cp node8 $(grep node8 gpurun_out/r6_bord_${v}_cp$i.txt | awk '{print $2}')"
+    timeout -k 10 300 python scratch/levels.py 40 3 > gpurun_out/r6_defer_${v}_p2$i.txt 2>&1
+    timeout -k 10 300 python scratch/levels_cfg.py CP 512 512 26 39 5 > gpurun_out/r6_defer_${v}_cp$i.txt 2>&1
+    echo "$v $i p2 node8 $(grep node8 gpurun_out/r6_defer_${v}_p2$i.txt | awk '{print $2}') cp node8 $(grep node8 gpurun_out/r6_defer_${v}_cp$i.txt | awk '{print $2}')"
   done
 done
 unset GPRX_LIB
-GPRX_LIB=scratch/var/libgprx_l8stamps.so timeout -k 10 200 python scratch/leaf8_timeline.py 40 > gpurun_out/r6_leaf_tl3.txt 2>&1
+GPRX_LIB=scratch/var/libgprx_l8stamps.so timeout -k 10 200 python scratch/leaf8_timeline.py 40 > gpurun_out/r6_leaf_tl4.txt 2>&1
 echo "diag ok"
