@@ -617,6 +617,40 @@ def test_cp_production_path_across_resident_rounds(gprx, ctx):
     b.close()
 
 
+def test_pinned_and_pageable_outputs_identical(gprx, ctx, golden_dir):
+    """The predictive mean / variance reach a page-locked caller buffer by one pitched DMA copy
+    (GPBatch allocates its outputs pinned) and a pageable one through the batch's staging buffer:
+    the same values either way, from gprx_batch_run and gprx_batch_predict."""
+    from gprx import _lib as L
+    from gprx.batch import host_empty
+
+    z = np.load(golden_dir / "p2_n256.npz")
+    X, Y, th, Xs = z["X"], z["Y"], z["theta"], z["Xs"]
+    G, M = Y.shape[0], Xs.shape[1]
+    b = gprx.GPBatch(G, X.shape[0], X.shape[1], M, ctx=ctx)
+    b.set_train(X, Y)
+    b.set_test(Xs)
+    T = np.ascontiguousarray(np.tile(th, (G, 1)))
+    pin_mu, pin_var = host_empty((G, M)), host_empty((G, M))
+    mu, var = np.empty((G, M)), np.empty((G, M))
+    mll = np.empty(G)
+    st, info = np.empty(G, dtype=np.int32), np.empty(G, dtype=np.int32)
+    for m_, v_ in ((mu, var), (pin_mu, pin_var)):
+        assert L.lib.gprx_batch_run(b.h, L.dptr(T), L.WANT_PREDICT, L.dptr(mll), None, L.dptr(m_), L.dptr(v_), L.iptr(st),
+                                    L.iptr(info)) == L.OK
+    np.testing.assert_array_equal(mu, pin_mu)
+    np.testing.assert_array_equal(var, pin_var)
+    r = b.run(T, grad=False, predict=True)
+    np.testing.assert_array_equal(r["mu"], mu)
+    np.testing.assert_array_equal(r["var"], var)
+    pm, pv = b.predict()
+    np.testing.assert_array_equal(pm, mu)
+    np.testing.assert_array_equal(pv, var)
+    assert L.lib.gprx_batch_predict(b.h, L.dptr(mu), L.dptr(var)) == L.OK
+    np.testing.assert_array_equal(mu, pm)
+    b.close()
+
+
 def test_batch_bytes_match_the_allocation(gprx, ctx):
     """gprx_batch_bytes (the chunk planner's size) against the device memory a batch actually takes
     (hipMemGetInfo before and after gprx_batch_create): equal up to the allocator's rounding."""
