@@ -10,3 +10,7 @@ timeout -k 10 400 python bench.py > gpurun_out/r6_bench1.json 2> gpurun_out/r6_b
 echo "bench ok"
 timeout -k 10 300 python scratch/levels.py 40 3 > gpurun_out/r6_levels.txt 2>&1
 echo "levels ok"
+rc=0; timeout -k 10 120 python bench.py --gpus 2 --no-cpu --no-opt > gpurun_out/r6_bench2_refused.txt 2>&1 || rc=$?
+echo "bench --gpus 2 on one GPU: rc=$rc (expected 2)"
+timeout -k 10 600 python bench.py --gpus 2 --rehearse --steps 3 --warmup 1 --no-cpu --no-opt > gpurun_out/r6_bench2.json 2> gpurun_out/r6_bench2.err
+echo "2-rank rehearsal ok"
