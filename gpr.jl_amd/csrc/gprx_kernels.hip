@@ -2375,6 +2375,64 @@ __device__ __forceinline__ void mma_rd(d4 (&acc)[QM], const double* __restrict__
   }
   if (it < nst) frag16_mma_rd(acc, f0);
 }
+// Row-packed mma_rd, for products whose output row order is free (the leaf's SYRK items): block a =
+// (h = a / 2, p = a % 2) holds rows 32 h + 2 i + p (i = lk + 4 q in the C layout), so a lane's two
+// rows 32 h + 2 lr, + 1 of an M column arrive by one 16-B load: 8 A loads per 16-deep stage instead
+// of 16.  Every output element sums its k in mma_rd's order: the same results.
+struct Frag16p {
+  double2 a[4][2];
+  double b[4];
+};
+__device__ __forceinline__ void frag16p_load_rd(Frag16p& f, const double* pa, const double* pb, size_t sa, size_t sb) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) f.a[s][h] = *(const double2*)(pa + s * sa + 32 * h);
+    f.b[s] = pb[s * sb];
+  }
+}
+__device__ __forceinline__ void frag16p_mma_rd(d4 (&acc)[QM], const Frag16p& f) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      acc[2 * h] = mfma(f.a[s][h].x, f.b[s], acc[2 * h]);
+      acc[2 * h + 1] = mfma(f.a[s][h].y, f.b[s], acc[2 * h + 1]);
+    }
+}
+// M's rows in pairs (16-B aligned: M's offset and ldm even)
+__device__ __forceinline__ void mma_rd_pk(d4 (&acc)[QM], const double* __restrict__ M, size_t ldm, const double* __restrict__ N,
+                                          size_t ldn, int K) {
+  const int nst = __builtin_amdgcn_readfirstlane(K >> 4);
+  if (nst <= 0) return;
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  const double* pa = M + 2 * lr + (size_t)lk * ldm;
+  const double* pb = N + lr + (size_t)lk * ldn;
+  const size_t sa = 4 * ldm, sb = 4 * ldn;
+  Frag16p f0, f1;
+  frag16p_load_rd(f0, pa, pb, sa, sb);
+  int it = 0;
+  for (; it + 1 < nst; it += 2) {
+    __builtin_amdgcn_sched_barrier(0);
+    frag16p_load_rd(f1, pa + (size_t)(it + 1) * 4 * sa, pb + (size_t)(it + 1) * 4 * sb, sa, sb);
+    frag16p_mma_rd(acc, f0);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x020, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (it + 2 < nst) frag16p_load_rd(f0, pa + (size_t)(it + 2) * 4 * sa, pb + (size_t)(it + 2) * 4 * sb, sa, sb);
+    frag16p_mma_rd(acc, f1);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x020, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (it < nst) frag16p_mma_rd(acc, f0);
+}
 __device__ __forceinline__ void acc_zero4(d4 (&acc)[QM]) {
 #pragma unroll
   for (int a = 0; a < QM; ++a) acc[a] = (d4){0.0, 0.0, 0.0, 0.0};
@@ -2463,6 +2521,9 @@ __device__ __forceinline__ void leaf9_body(const DevBatch& db, int o, int upd) {
     if (cw >= 0) preload(0);
 #ifndef GPRX_L9_BORDER
 #define GPRX_L9_BORDER 1
+#endif
+#ifndef GPRX_L9_PK
+#define GPRX_L9_PK 1
 #endif
     // phase B (and the held inverse items): round-robin position.  BORDER 1: waves 4, 1, 2, 3 first
     // (wave 4 alone on its SIMD while wave 0 waits; waves 5-7 share SIMDs with the older waves 1-3,
@@ -2636,6 +2697,21 @@ __device__ __forceinline__ void leaf9_body(const DevBatch& db, int o, int upd) {
           // S(ti, tj) rows xq..: OUT[x][xq + lr] = S[xq + lr][x], M = L(tj, kk), N = L(ti, kk) rows xq..
           // (a diagonal tile's blocks above the diagonal are formed and stored too: no reader uses them)
           d4 acc[QM];
+#if GPRX_L9_PK
+          // row-packed core: block a holds OUT rows 32 (a / 2) + (a % 2) + 2 lk + 8 q
+          const int lop = 2 * lk * ldi + lr;
+#pragma unroll
+          for (int a = 0; a < QM; ++a)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              acc[a][q] = -Kc[(tj * TS + 32 * (a >> 1) + (a & 1) + 8 * q) * ldi + ti * TS + xq + lop];
+          mma_rd_pk(acc, Lw + (size_t)kk * TS * ld + tj * TS, ld, Lw + (size_t)kk * TS * ld + ti * TS + xq, ld, TS);
+#pragma unroll
+          for (int a = 0; a < QM; ++a)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              S[(tj * TS + 32 * (a >> 1) + (a & 1) + 8 * q) * ldi + ti * TS + xq + lop] = -acc[a][q];
+#else
 #pragma unroll
           for (int a = 0; a < QM; ++a)
 #pragma unroll
@@ -2645,6 +2721,7 @@ __device__ __forceinline__ void leaf9_body(const DevBatch& db, int o, int upd) {
           for (int a = 0; a < QM; ++a)
 #pragma unroll
             for (int q = 0; q < 4; ++q) S[(tj * TS + 16 * a + 4 * q) * ldi + ti * TS + xq + lo] = -acc[a][q];
+#endif
           W_TS(8 * k + 1 + (nb < 5 ? nb++ : 5));
         };
         for (int g = rw < 0 ? nc4 : rw; g < nc4; g += L9_HWB) {

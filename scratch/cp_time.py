@@ -1,9 +1,9 @@
 """CP (N=512, d=26, all 26 outputs) per-kernel times per batch for leaf / small_n choices."""
-import sys, time
+import os, sys, time
 sys.path[:0] = ['/root/repo', '/root/repo/gpr.jl_amd']
 import numpy as np, gprx
 from gprx import data
-trials = 16
+trials = int(os.environ.get('CP_TRIALS', 16))
 trs = [data.make_trial('CP', 512, 100, seed=data.trial_seed('CP', t)) for t in range(trials)]
 X = np.stack([tr['X'] for tr in trs for _ in range(26)]); Y = np.concatenate([tr['Xcurr'] for tr in trs])
 XT = np.stack([tr['Xs'] for tr in trs for _ in range(26)])
