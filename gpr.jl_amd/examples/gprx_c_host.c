@@ -48,6 +48,11 @@ int main(int argc, char** argv) {
     fprintf(stderr, "usage: %s trial.cst theta.f64 xs.f64 M\n", argv[0]);
     return 2;
   }
+  if (gprx_abi_version() != GPRX_ABI_VERSION) {
+    fprintf(stderr, "libgprx implements ABI version %d, this host was built against %d\n", gprx_abi_version(),
+            GPRX_ABI_VERSION);
+    return 2;
+  }
   /* GPRXCST1 header: magic[8], u32 d, u32 G, u64 N, u64 reserved */
   FILE* f = fopen(argv[1], "rb");
   if (!f) return fail("open trial", GPRX_INVALID_ARGUMENT, NULL);

@@ -12,6 +12,10 @@ import pathlib
 _HERE = pathlib.Path(__file__).resolve().parent
 LIB_PATH = pathlib.Path(os.environ.get("GPRX_LIB", _HERE.parent / "lib" / "libgprx.so"))
 
+# the header's GPRX_ABI_VERSION this binding is written against (include/gprx.h); the loader refuses
+# a library that reports another one (a variant build selected by GPRX_LIB skips the build-id check)
+ABI_VERSION = 3
+
 OK = 0
 NOT_POSITIVE_DEFINITE = 1
 INVALID_ARGUMENT = 2
@@ -115,6 +119,9 @@ def _load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    abi = lib.gprx_abi_version()
+    if abi != ABI_VERSION:
+        raise ImportError(f"gprx: {LIB_PATH} implements ABI version {abi}, this binding expects {ABI_VERSION}")
     want = source_build_id()
     got = lib.gprx_build_id().decode()
     if want is not None and got != want:

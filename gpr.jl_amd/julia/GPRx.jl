@@ -24,7 +24,13 @@ using GaussianProcesses: GPE, SEArd, Mean
 using LinearAlgebra
 
 const LIB = joinpath(@__DIR__, "..", "lib", "libgprx.so")
+const ABI = Cint(3)  # include/gprx.h GPRX_ABI_VERSION these ccall signatures follow
 const OK, NOT_PD, INVALID = Cint(0), Cint(1), Cint(2)
+
+function __init__()
+    abi = ccall((:gprx_abi_version, LIB), Cint, ())
+    abi == ABI || error("gprx: $LIB implements ABI version $abi, GPRx.jl expects $ABI")
+end
 
 # one context (HIP stream) per Julia thread; device = thread mod #GPUs (core.jl:28 workers), the
 # device count from the library (GPRX_NGPU, if set, caps it, e.g. to leave GPUs to other jobs)

@@ -10,7 +10,8 @@ import pytest
 from gprx import _lib as L
 from oracle import gp_oracle as O
 
-HEADER = pathlib.Path(__file__).resolve().parents[1] / "include" / "gprx.h"
+REPO = pathlib.Path(__file__).resolve().parents[1]
+HEADER = REPO / "include" / "gprx.h"
 
 
 def declared_functions():
@@ -32,6 +33,11 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_status_strings():
     assert L.lib.gprx_abi_version() == 3
+    # the bindings' constants follow the header
+    hdr = (REPO / "include" / "gprx.h").read_text()
+    assert f"#define GPRX_ABI_VERSION {L.ABI_VERSION}\n" in hdr
+    jl = (REPO / "gpr.jl_amd" / "julia" / "GPRx.jl").read_text()
+    assert f"const ABI = Cint({L.ABI_VERSION})" in jl
     assert L.lib.gprx_status_string(1) == b"not positive definite"
 
 
